@@ -1,0 +1,77 @@
+"""Build libc2d_hip.so (gfx950) in-tree with hipcc.
+
+Usage: python -m clap2diffusion_amd.build [--force] [--jobs N]
+The shared library lands next to this file so it travels with the repo
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libc2d_hip.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+         "-Wno-unused-result", "-I", str(ROOT / "include")]
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    for f in sorted(CSRC.iterdir()):
+        if f.suffix in (".hip", ".h", ".cpp"):
+            h.update(f.name.encode())
+            h.update(f.read_bytes())
+    h.update((ROOT / "include" / "c2d.h").read_bytes())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: str, build_dir: Path) -> Path:
+    obj = build_dir / (Path(src).stem + ".o")
+    cmd = [HIPCC, *FLAGS, "-c", str(CSRC / src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
+    stamp = PKG / ".libc2d_hip.stamp"
+    dig = _digest()
+    if LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig and not force:
+        if verbose:
+            print(f"[c2d] {LIB.name} up to date ({dig})")
+        return LIB
+    build_dir = ROOT / "build" / "c2d"
+    build_dir.mkdir(parents=True, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, build_dir), SOURCES))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    stamp.write_text(dig)
+    if verbose:
+        print(f"[c2d] built {LIB} ({dig})")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=4)
+    a = ap.parse_args()
+    build(force=a.force, jobs=a.jobs)
+    sys.exit(0)

@@ -1,0 +1,321 @@
+// Flash-style attention forward for gfx950 (MFMA f32_16x16x32_f16) and the
+// HTSAT Swin window attention.
+//
+// attention_fwd: one workgroup = 4 waves = 128 queries of one (batch, head);
+// each wave owns 32 queries (two 16-query groups).  Key/value tiles of 64 keys
+// are register-staged into LDS (K rows padded to an odd number of 16-B slots,
+// V rows padded for conflict-free ds_read_b64_tr_b16).  Scores are computed
+// transposed, S^T = K Q^T, so each lane holds 16 keys of ONE query: the softmax
+// row max needs two lane shuffles, the row sum none until the end, and the
+// exponentiated P fragment is already the B operand of O^T = V^T P^T (the k
+// order of the PV product is permuted to match, V^T comes from the transposed
+// LDS read).  O^T accumulators keep the query on the lane, so the online-softmax
+// rescale is lane-local.  Softmax in fp32 with exp2 and a folded log2(e) scale.
+#include "common.h"
+
+namespace c2d {
+
+template <int D> struct AttnCfg {
+    static constexpr int DP = (D + 31) / 32 * 32;      // K dim of QK^T, multiple of 32
+    static constexpr int DV = (D + 15) / 16 * 16;      // N dim of PV, multiple of 16
+    static constexpr int NDC = DP / 32;
+    static constexpr int NDT = DV / 16;
+    static constexpr int KS = DP * 2 + 16;             // K row stride (bytes): odd # of 16-B slots
+    static constexpr int VS = (DV == 48) ? 96 : (DV == 64 || DV == 80) ? 160 : (DV == 160) ? 352 : DV * 2 + 32;
+    static constexpr int DCH = D / 8;                  // real 16-B chunks per row
+    static constexpr int NLD = (64 * DCH + 255) / 256; // staged chunks per thread per tile
+    static constexpr int K_BYTES = 64 * KS;
+    static constexpr int V_BYTES = 64 * VS;
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
+                                                       int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
+                                                       int ldo, int heads, int lq, int lk, float scale_log2,
+                                                       int kv_div, int nqb) {
+    using C = AttnCfg<D>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ks = smem;
+    char* Vs = smem + C::K_BYTES;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = tile / nqb, qb = tile - bh * nqb;
+    const int b = bh / heads, h = bh - b * heads;
+    const int bk = b / kv_div;
+    const int q0 = qb * 128 + wave * 32;
+    const int g = lane >> 4, li = lane & 15;
+
+    // zero the K padding columns once (never rewritten) and the V pad columns
+    for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 256) {
+        int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
+        *reinterpret_cast<f16x8*>(Ks + row * C::KS + ch * 16) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 256) {
+        int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
+        *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+
+    // Q fragments (B operand of S^T = K Q^T): query q0 + 16 qg + li, d = 32 dc + 8 g .. +7
+    f16x8 qf[2][C::NDC];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+        const int qi = q0 + qg * 16 + li;
+#pragma unroll
+        for (int dc = 0; dc < C::NDC; ++dc) {
+            const int d0 = dc * 32 + g * 8;
+            if (qi < lq && d0 < D)
+                qf[qg][dc] = *reinterpret_cast<const f16x8*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
+            else
+                qf[qg][dc] = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    f32x4 acc[C::NDT][2];
+#pragma unroll
+    for (int dt = 0; dt < C::NDT; ++dt)
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) acc[dt][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+
+    const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
+    const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
+    f16x8 rk[C::NLD], rv[C::NLD];
+    auto gload = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            const int idx = tid + 256 * i;
+            const int row = idx / C::DCH, ch = idx - row * C::DCH;
+            const int key = t * 64 + row;
+            if (idx < 64 * C::DCH && key < lk) {
+                rk[i] = *reinterpret_cast<const f16x8*>(kbase + (size_t)key * ldk + ch * 8);
+                rv[i] = *reinterpret_cast<const f16x8*>(vbase + (size_t)key * ldv + ch * 8);
+            } else {
+                rk[i] = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+                rv[i] = rk[i];
+            }
+        }
+    };
+    auto swrite = [&]() {
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            const int idx = tid + 256 * i;
+            if (idx < 64 * C::DCH) {
+                const int row = idx / C::DCH, ch = idx - row * C::DCH;
+                *reinterpret_cast<f16x8*>(Ks + row * C::KS + ch * 16) = rk[i];
+                *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = rv[i];
+            }
+        }
+    };
+
+    const int ntiles = (lk + 63) / 64;
+    gload(0);
+    __syncthreads();  // pad zeroing done before the first tile lands
+    swrite();
+    __syncthreads();
+
+    for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) gload(t + 1);
+
+        // ---- S^T tiles: s[qg][kg] holds keys 16 kg + 4 g + r of query li
+        f32x4 s[2][4];
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg) s[qg][kg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg) {
+#pragma unroll
+            for (int dc = 0; dc < C::NDC; ++dc) {
+                const f16x8 kf = *reinterpret_cast<const f16x8*>(Ks + (kg * 16 + li) * C::KS + (dc * 4 + g) * 16);
+#pragma unroll
+                for (int qg = 0; qg < 2; ++qg)
+                    s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], s[qg][kg], 0, 0, 0);
+            }
+        }
+        if ((t + 1) * 64 > lk) {  // tail tile: mask keys >= lk
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = t * 64 + kg * 16 + g * 4 + r;
+                    if (key >= lk) { s[0][kg][r] = -1e30f; s[1][kg][r] = -1e30f; }
+                }
+        }
+
+        // ---- online softmax (log2 domain), P packed to fp16 B fragments
+        f16x8 pf[2][2];
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) {
+            float mx = s[qg][0][0];
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qg][kg][r]);
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float m_new = fmaxf(m_run[qg], mx * scale_log2);
+            const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_new);
+            m_run[qg] = m_new;
+            float rs = 0.f;
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pv = __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], scale_log2, -m_new));
+                    s[qg][kg][r] = pv;
+                    rs += pv;
+                }
+            l_run[qg] = l_run[qg] * alpha + rs;
+#pragma unroll
+            for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    pf[qg][kb][j] = (f16)s[qg][2 * kb][j];
+                    pf[qg][kb][4 + j] = (f16)s[qg][2 * kb + 1][j];
+                }
+            }
+        }
+
+        // ---- O^T += V^T P^T ; V^T fragment via transposed LDS reads
+#pragma unroll
+        for (int dt = 0; dt < C::NDT; ++dt) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const int qq = li >> 2, pp = li & 3;
+                const int row1 = kb * 32 + g * 4 + qq;
+                const char* a1 = Vs + row1 * C::VS + (dt * 16 + pp * 4) * 2;
+                const char* a2 = a1 + 16 * C::VS;
+                s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a1);
+                s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a2);
+                f16x8 vf;
+                f16x4 h1 = __builtin_bit_cast(f16x4, t1), h2 = __builtin_bit_cast(f16x4, t2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { vf[j] = h1[j]; vf[4 + j] = h2[j]; }
+#pragma unroll
+                for (int qg = 0; qg < 2; ++qg)
+                    acc[dt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[qg][kb], acc[dt][qg], 0, 0, 0);
+            }
+        }
+
+        if (t + 1 < ntiles) {
+            __syncthreads();
+            swrite();
+            __syncthreads();
+        }
+    }
+
+    // ---- epilogue: lane holds O[query li][d = 16 dt + 4 g + r]
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+        float l = l_run[qg];
+        l += __shfl_xor(l, 16);
+        l += __shfl_xor(l, 32);
+        const float inv = 1.0f / l;
+        const int qi = q0 + qg * 16 + li;
+        if (qi >= lq) continue;
+        f16* orow = o + ((size_t)b * lq + qi) * ldo + h * D;
+#pragma unroll
+        for (int dt = 0; dt < C::NDT; ++dt) {
+            const int d0 = dt * 16 + g * 4;
+            if (d0 < D) {
+                f16x4 ov;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ov[r] = (f16)(acc[dt][qg][r] * inv);
+                *reinterpret_cast<f16x4*>(orow + d0) = ov;
+            }
+        }
+    }
+}
+
+template <int D>
+static int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                       int batch, int heads, int lq, int lk, float scale, int kv_div, hipStream_t s) {
+    using C = AttnCfg<D>;
+    const int nqb = (lq + 127) / 128;
+    const int smem = C::K_BYTES + C::V_BYTES;
+    dim3 grid(nqb * batch * heads);
+    hipLaunchKernelGGL((attn_fwd_kernel<D>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
+                       (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
+    return check_launch();
+}
+
+// ------------------------------------------------------------ window attention
+// one workgroup of 64 threads per (window, head); thread = query.  d <= 32.
+__global__ void __launch_bounds__(64) window_attn_kernel(const f16* __restrict__ qkv, int ld, const int* __restrict__ row_map,
+                                                         int heads, int d, const float* __restrict__ bias,
+                                                         const float* __restrict__ mask, int n_mask,
+                                                         f16* __restrict__ out, int ldo, float scale) {
+    __shared__ float Ks[64][33];
+    __shared__ float Vs[64][33];
+    const int w = blockIdx.x / heads, h = blockIdx.x - (blockIdx.x / heads) * heads;
+    const int t = threadIdx.x;
+    const int C = heads * d;
+    const int row = row_map[w * 64 + t];
+    const f16* base = qkv + (size_t)row * ld;
+    float qv[32];
+    for (int i = 0; i < d; ++i) {
+        qv[i] = (float)base[h * d + i] * scale;
+        Ks[t][i] = (float)base[C + h * d + i];
+        Vs[t][i] = (float)base[2 * C + h * d + i];
+    }
+    __syncthreads();
+    const float* brow = bias + ((size_t)h * 64 + t) * 64;
+    const float* mrow = mask ? mask + ((size_t)(w % n_mask) * 64 + t) * 64 : nullptr;
+    float sc[64];
+    float mx = -1e30f;
+    for (int j = 0; j < 64; ++j) {
+        float a = 0.f;
+        for (int i = 0; i < d; ++i) a = fmaf(qv[i], Ks[j][i], a);
+        a += brow[j];
+        if (mrow) a += mrow[j];
+        sc[j] = a;
+        mx = fmaxf(mx, a);
+    }
+    float l = 0.f;
+    for (int j = 0; j < 64; ++j) { sc[j] = __expf(sc[j] - mx); l += sc[j]; }
+    const float inv = 1.0f / l;
+    f16* orow = out + (size_t)row * ldo + h * d;
+    for (int i = 0; i < d; ++i) {
+        float a = 0.f;
+        for (int j = 0; j < 64; ++j) a = fmaf(sc[j], Vs[j][i], a);
+        orow[i] = (f16)(a * inv);
+    }
+}
+
+}  // namespace c2d
+
+using namespace c2d;
+
+extern "C" int c2d_attention_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                                 int ldo, int batch, int heads, int lq, int lk, int d, float scale, int kv_div,
+                                 void* stream) {
+    if (!q || !k || !v || !o || kv_div <= 0) return C2D_E_ARG;
+    if (batch <= 0 || heads <= 0 || lq <= 0 || lk <= 0) return C2D_E_SHAPE;
+    if ((ldq & 7) || (ldk & 7) || (ldv & 7) || (ldo & 3)) return C2D_E_ALIGN;
+    if (!aligned16(q) || !aligned16(k) || !aligned16(v) || ((uintptr_t)o & 7)) return C2D_E_ALIGN;
+    if (heads * d > ldq || heads * d > ldk || heads * d > ldv || heads * d > ldo) return C2D_E_SHAPE;
+    hipStream_t s = (hipStream_t)stream;
+    switch (d) {
+        case 40: return launch_attn<40>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, s);
+        case 64: return launch_attn<64>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, s);
+        case 80: return launch_attn<80>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, s);
+        case 160: return launch_attn<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, s);
+        default: return C2D_E_SHAPE;
+    }
+}
+
+extern "C" int c2d_window_attention(const void* qkv, int ld_qkv, const int* row_map, int n_windows, int heads, int d,
+                                    const float* bias, const float* mask, int n_mask, void* out, int ldo,
+                                    void* stream) {
+    if (!qkv || !row_map || !bias || !out) return C2D_E_ARG;
+    if (d <= 0 || d > 32 || heads <= 0 || n_windows <= 0) return C2D_E_SHAPE;
+    if (mask && n_mask <= 0) return C2D_E_ARG;
+    if (ld_qkv < 3 * heads * d || ldo < heads * d) return C2D_E_SHAPE;
+    hipLaunchKernelGGL(window_attn_kernel, dim3(n_windows * heads), dim3(64), 0, (hipStream_t)stream,
+                       (const f16*)qkv, ld_qkv, row_map, heads, d, bias, mask, n_mask, (f16*)out, ldo,
+                       1.0f / sqrtf((float)d));
+    return check_launch();
+}

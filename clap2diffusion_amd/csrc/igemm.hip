@@ -1,0 +1,369 @@
+// Implicit-GEMM convolution / linear kernel for gfx950 (MFMA f32_16x16x32_f16).
+//
+//   out[m, j] = act(sum_k A[m, k] W[j, k] + bias[j]) + temb[n(m), j] + resid[m, j]
+//
+// A = on-the-fly im2col of an NHWC fp16 input (optionally two channel sources,
+// i.e. the UNet skip concat, and optionally a nearest-x2 upsampled view), with a
+// fused prologue (GroupNorm affine [+SiLU], LayerNorm, or SiLU) applied to the
+// in-bounds elements only, so zero padding stays zero after normalisation as in
+// torch (conv pads the *normalised* tensor).  W = packed [cout][kpad] fp16.
+//
+// Tiling: BM x BN block tile (128x128 or 64x64), BK = 64, 256 threads = 4 waves
+// in 2x2, each wave (BM/2)x(BN/2) of 16x16 MFMA tiles.  The MFMA computes the
+// transposed product D^T = W . A^T so every lane ends with 4 consecutive output
+// columns of one row: the epilogue stores 8-byte row segments straight to HBM.
+// A and B tiles are register-staged (load early, transform, ds_write_b128 late)
+// into a double-buffered, XOR-swizzled LDS image: one barrier per K step.
+#include "common.h"
+
+namespace c2d {
+
+enum AMode { AM_1X1 = 0, AM_3X3_FAST = 1, AM_3X3_GEN = 2 };
+
+struct IgemmParams {
+    const f16* src0; const f16* src1; int c0, c1, cin;
+    int n, h, w, oh, ow, stride, up, pad;
+    int vh, vw;  // virtual (possibly upsampled) input size
+    const f16* wt; int cout, kpad, ktot;
+    int pro, pro_silu;
+    const float* pro_a; const float* pro_b; const float* gamma; const float* beta;
+    const float* bias; int act;
+    const f16* temb; int temb_ld;
+    const f16* resid; int resid_ld;
+    f16* out; int out_ld;
+    int M;       // rows = n*oh*ow
+    int gx, gy;  // tiles along cout / M
+};
+
+// byte offset of 16-byte chunk `c` (0..7) of `row` in a [rows][64] fp16 LDS tile
+__device__ __forceinline__ int lds_off(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+
+template <int BM>
+struct RowInfo {
+    int n[BM / 32], iy[BM / 32], ix[BM / 32];
+    bool ok[BM / 32];
+};
+
+__device__ __forceinline__ f16x8 zero8() {
+    f16x8 z;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] = (f16)0.f;
+    return z;
+}
+
+// Load one 16-B chunk of A (8 channels) for output row described by (n, iy, ix)
+template <int AMODE>
+__device__ __forceinline__ f16x8 load_a_chunk(const IgemmParams& p, int n, int iy0, int ix0, bool rok,
+                                              int k, int tap_fast, int cbase_fast, int cc, int& cout_c,
+                                              bool& valid) {
+    int c, ky, kx;
+    if (AMODE == AM_1X1) {
+        c = k; ky = 0; kx = 0;
+        valid = rok && (c < p.cin);
+    } else if (AMODE == AM_3X3_FAST) {
+        c = cbase_fast + cc * 8;
+        ky = tap_fast / 3; kx = tap_fast - ky * 3;
+        valid = rok;
+    } else {
+        int tap = k / p.cin;
+        c = k - tap * p.cin;
+        ky = tap / 3; kx = tap - ky * 3;
+        valid = rok && (tap < 9);
+    }
+    int iy = iy0 + ky, ix = ix0 + kx;
+    valid = valid && iy >= 0 && iy < p.vh && ix >= 0 && ix < p.vw;
+    cout_c = c;
+    if (!valid) return zero8();
+    if (p.up) { iy >>= 1; ix >>= 1; }
+    size_t pix = ((size_t)n * p.h + iy) * p.w + ix;
+    const f16* ptr = (c < p.c0) ? (p.src0 + pix * p.c0 + c) : (p.src1 + pix * p.c1 + (c - p.c0));
+    return *reinterpret_cast<const f16x8*>(ptr);
+}
+
+__device__ __forceinline__ f16x8 apply_pro(const IgemmParams& p, f16x8 v, int n, int m, int c) {
+    if (p.pro == C2D_PRO_GN) {
+        const float4* sc = reinterpret_cast<const float4*>(p.pro_a + (size_t)n * p.cin + c);
+        const float4* sh = reinterpret_cast<const float4*>(p.pro_b + (size_t)n * p.cin + c);
+        float4 s0 = sc[0], s1 = sc[1], h0 = sh[0], h1 = sh[1];
+        float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float y = (float)v[i] * s[i] + hh[i];
+            if (p.pro_silu) y = silu_f(y);
+            v[i] = (f16)y;
+        }
+    } else if (p.pro == C2D_PRO_LN) {
+        float2 st = *reinterpret_cast<const float2*>(p.pro_a + (size_t)m * 2);
+        const float4* g = reinterpret_cast<const float4*>(p.gamma + c);
+        const float4* b = reinterpret_cast<const float4*>(p.beta + c);
+        float4 g0 = g[0], g1 = g[1], b0 = b[0], b1 = b[1];
+        float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (f16)(((float)v[i] - st.x) * st.y * gg[i] + bb[i]);
+    } else if (p.pro == C2D_PRO_SILU) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (f16)silu_f((float)v[i]);
+    }
+    return v;
+}
+
+template <int BM, int BN, int AMODE>
+__global__ void __launch_bounds__(256) igemm_kernel(IgemmParams p) {
+    constexpr int TM = BM / 32;  // 16-row MFMA tiles per wave along M
+    constexpr int TN = BN / 32;  // along N
+    constexpr int ACH = BM / 32; // A chunks per thread per K step
+    constexpr int BCH = BN / 32;
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tile = xcd_remap(blockIdx.x, p.gx * p.gy);
+    const int mt = tile / p.gx, nt = tile - mt * p.gx;
+    const int m0 = mt * BM, n0 = nt * BN;
+
+    // per-thread staging rows (fixed across K): chunk cc, rows tid/8 + 32 i
+    const int cc = tid & 7;
+    const int hw = p.oh * p.ow;
+    int a_n[ACH], a_iy[ACH], a_ix[ACH], a_m[ACH];
+    bool a_ok[ACH];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+        int m = m0 + (tid >> 3) + 32 * i;
+        a_m[i] = m;
+        a_ok[i] = m < p.M;
+        int mm = a_ok[i] ? m : 0;
+        int nn = mm / hw, r = mm - nn * hw;
+        int oy = r / p.ow, ox = r - oy * p.ow;
+        a_n[i] = nn;
+        a_iy[i] = oy * p.stride - p.pad;
+        a_ix[i] = ox * p.stride - p.pad;
+    }
+    const f16* b_ptr[BCH];
+    bool b_ok[BCH];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+        int j = n0 + (tid >> 3) + 32 * i;
+        b_ok[i] = j < p.cout;
+        b_ptr[i] = p.wt + (size_t)(b_ok[i] ? j : 0) * p.kpad + cc * 8;
+    }
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    f16x8 ra[ACH], rb[BCH];
+    int rc[ACH];
+    bool rv[ACH];
+    const int nk = p.kpad / 64;
+
+    auto gload = [&](int kt) {
+        const int k0 = kt * 64;
+        int tap = 0, cbase = 0;
+        if (AMODE == AM_3X3_FAST) { tap = k0 / p.cin; cbase = k0 - tap * p.cin; }
+#pragma unroll
+        for (int i = 0; i < ACH; ++i)
+            ra[i] = load_a_chunk<AMODE>(p, a_n[i], a_iy[i], a_ix[i], a_ok[i], k0 + cc * 8, tap, cbase, cc, rc[i], rv[i]);
+#pragma unroll
+        for (int i = 0; i < BCH; ++i)
+            rb[i] = b_ok[i] ? *reinterpret_cast<const f16x8*>(b_ptr[i] + k0) : zero8();
+    };
+    auto swrite = [&](int buf) {
+        char* As = smem + buf * (A_BYTES + B_BYTES);
+        char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) {
+            f16x8 v = ra[i];
+            if (p.pro != C2D_PRO_NONE && rv[i]) v = apply_pro(p, v, a_n[i], a_m[i], rc[i]);
+            int row = (tid >> 3) + 32 * i;
+            *reinterpret_cast<f16x8*>(As + lds_off(row, cc)) = v;
+        }
+#pragma unroll
+        for (int i = 0; i < BCH; ++i) {
+            int row = (tid >> 3) + 32 * i;
+            *reinterpret_cast<f16x8*>(Bs + lds_off(row, cc)) = rb[i];
+        }
+    };
+
+    gload(0);
+    swrite(0);
+    __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) gload(kt + 1);
+        const char* As = smem + buf * (A_BYTES + B_BYTES);
+        const char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + (lane >> 4);
+            f16x8 fa[TM], fb[TN];
+#pragma unroll
+            for (int t = 0; t < TM; ++t) {
+                int row = wm * (BM / 2) + t * 16 + (lane & 15);
+                fa[t] = *reinterpret_cast<const f16x8*>(As + lds_off(row, ch));
+            }
+#pragma unroll
+            for (int t = 0; t < TN; ++t) {
+                int row = wn * (BN / 2) + t * 16 + (lane & 15);
+                fb[t] = *reinterpret_cast<const f16x8*>(Bs + lds_off(row, ch));
+            }
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+        }
+        if (kt + 1 < nk) swrite(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane holds out[row = m-tile row (lane&15)][cols 4*(lane>>4) .. +3]
+    const bool geglu = (p.act == C2D_ACT_GEGLU);
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+        const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
+        if (m >= p.M) continue;
+        const int nimg = m / hw;
+        if (!geglu) {
+#pragma unroll
+            for (int a = 0; a < TN; ++a) {
+                const int j = n0 + wn * (BN / 2) + a * 16 + 4 * (lane >> 4);
+                if (j >= p.cout) continue;
+                float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+                if (p.bias) {
+                    float4 bb = *reinterpret_cast<const float4*>(p.bias + j);
+                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
+                    else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+                    else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
+                }
+                if (p.temb) {
+                    f16x4 t = *reinterpret_cast<const f16x4*>(p.temb + (size_t)nimg * p.temb_ld + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                if (p.resid) {
+                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                f16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+            }
+        } else {
+            // packed rows: [16 h | 16 g] per 32-row block -> 16 output features
+#pragma unroll
+            for (int a = 0; a < TN; a += 2) {
+                const int jp = n0 + wn * (BN / 2) + a * 16;  // packed row of the h block
+                if (jp >= p.cout) continue;
+                const int jo = (jp >> 1) + 4 * (lane >> 4);  // output feature
+                const int jh = jp + 4 * (lane >> 4), jg = jh + 16;
+                float hv[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+                float gv[4] = {acc[a + 1][b][0], acc[a + 1][b][1], acc[a + 1][b][2], acc[a + 1][b][3]};
+                if (p.bias) {
+                    float4 bh = *reinterpret_cast<const float4*>(p.bias + jh);
+                    float4 bg = *reinterpret_cast<const float4*>(p.bias + jg);
+                    hv[0] += bh.x; hv[1] += bh.y; hv[2] += bh.z; hv[3] += bh.w;
+                    gv[0] += bg.x; gv[1] += bg.y; gv[2] += bg.z; gv[3] += bg.w;
+                }
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = hv[r] * gelu_f(gv[r]);
+                if (p.resid) {
+                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + jo);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                f16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + jo) = o;
+            }
+        }
+    }
+}
+
+template <int BM, int BN, int AMODE>
+static void launch(const IgemmParams& p, hipStream_t s) {
+    const int smem = 2 * (BM + BN) * 128;
+    dim3 grid(p.gx * p.gy);
+    hipLaunchKernelGGL((igemm_kernel<BM, BN, AMODE>), grid, dim3(256), smem, s, p);
+}
+
+}  // namespace c2d
+
+using namespace c2d;
+
+extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
+    if (!d || !d->src0 || !d->weight || !d->out) return C2D_E_ARG;
+    if (d->ksize != 1 && d->ksize != 3) return C2D_E_SHAPE;
+    if (d->c1 > 0 && !d->src1) return C2D_E_ARG;
+    const int cin = d->c0 + d->c1;
+    if ((d->c0 & 7) || (d->c1 & 7) || cin <= 0) return C2D_E_SHAPE;
+    if (d->kpad & 63) return C2D_E_SHAPE;
+    const int ktot = d->ksize * d->ksize * cin;
+    if (d->kpad < ktot) return C2D_E_SHAPE;
+    if ((d->cout & 3) || d->cout <= 0) return C2D_E_SHAPE;
+    if (d->act == C2D_ACT_GEGLU && (d->cout & 31)) return C2D_E_SHAPE;
+    if (d->act == C2D_ACT_GEGLU && d->temb) return C2D_E_ARG;
+    if (d->act != C2D_ACT_NONE && d->act != C2D_ACT_GEGLU && d->temb) return C2D_E_ARG;
+    if ((d->out_ld & 3) || (d->resid && (d->resid_ld & 3)) || (d->temb && (d->temb_ld & 3))) return C2D_E_ALIGN;
+    if (!aligned16(d->src0) || (d->src1 && !aligned16(d->src1)) || !aligned16(d->weight)) return C2D_E_ALIGN;
+    if (((uintptr_t)d->out & 7) || (d->resid && ((uintptr_t)d->resid & 7)) || (d->temb && ((uintptr_t)d->temb & 7)))
+        return C2D_E_ALIGN;
+    if (d->bias && ((uintptr_t)d->bias & 15)) return C2D_E_ALIGN;
+    if (d->pro == C2D_PRO_GN && (!d->pro_a || !d->pro_b || (cin & 3))) return C2D_E_ARG;
+    if (d->pro == C2D_PRO_LN && (!d->pro_a || !d->gamma || !d->beta)) return C2D_E_ARG;
+    if (d->pro < 0 || d->pro > 3 || d->act < 0 || d->act > 4) return C2D_E_ARG;
+    if (d->stride != 1 && d->stride != 2) return C2D_E_SHAPE;
+    if (d->ksize == 1 && (d->stride != 1 || d->up || d->oh != d->h || d->ow != d->w)) return C2D_E_SHAPE;
+    if (d->up && d->stride != 1) return C2D_E_SHAPE;
+
+    IgemmParams p;
+    p.src0 = (const f16*)d->src0; p.src1 = (const f16*)d->src1;
+    p.c0 = d->c0; p.c1 = d->c1; p.cin = cin;
+    p.n = d->n; p.h = d->h; p.w = d->w; p.oh = d->oh; p.ow = d->ow;
+    p.stride = d->stride; p.up = d->up; p.pad = (d->ksize == 3) ? 1 : 0;
+    p.vh = d->up ? 2 * d->h : d->h; p.vw = d->up ? 2 * d->w : d->w;
+    if (d->ksize == 3) {
+        int eh = (p.vh + 2 - 3) / d->stride + 1, ew = (p.vw + 2 - 3) / d->stride + 1;
+        if (eh != d->oh || ew != d->ow) return C2D_E_SHAPE;
+    }
+    p.wt = (const f16*)d->weight; p.cout = d->cout; p.kpad = d->kpad; p.ktot = ktot;
+    p.pro = d->pro; p.pro_silu = d->pro_silu;
+    p.pro_a = d->pro_a; p.pro_b = d->pro_b; p.gamma = d->gamma; p.beta = d->beta;
+    p.bias = d->bias; p.act = d->act;
+    p.temb = (const f16*)d->temb; p.temb_ld = d->temb_ld;
+    p.resid = (const f16*)d->resid; p.resid_ld = d->resid_ld;
+    p.out = (f16*)d->out; p.out_ld = d->out_ld;
+    p.M = d->n * d->oh * d->ow;
+    if (p.M <= 0) return C2D_OK;
+
+    hipStream_t s = (hipStream_t)stream;
+    const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
+    // small problems: 64x64 tiles to fill 256 CUs
+    const long tiles128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
+    const bool small = tiles128 < 512;
+    if (small) {
+        p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
+        if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);
+        else if (amode == AM_3X3_FAST) launch<64, 64, AM_3X3_FAST>(p, s);
+        else launch<64, 64, AM_3X3_GEN>(p, s);
+    } else {
+        p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
+        if (amode == AM_1X1) launch<128, 128, AM_1X1>(p, s);
+        else if (amode == AM_3X3_FAST) launch<128, 128, AM_3X3_FAST>(p, s);
+        else launch<128, 128, AM_3X3_GEN>(p, s);
+    }
+    return check_launch();
+}

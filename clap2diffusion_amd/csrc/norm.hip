@@ -1,0 +1,251 @@
+// GroupNorm statistics (folded into per-(image, channel) affine tables) and
+// LayerNorm statistics / apply for gfx950.  All HBM-bound: 16-B vector loads,
+// per-block LDS reduction, one fp32 atomic per (block, channel, moment).
+#include "common.h"
+
+namespace c2d {
+
+// ---------------------------------------------------------------- GroupNorm
+// ws layout: fp32 [n][cin][2] shifted moments (sum(x-s_g), sum((x-s_g)^2)).
+// The per-group shift s_g = x[n, pixel 0, first channel of g] keeps the
+// one-pass variance well conditioned when |mean| >> std.
+__device__ __forceinline__ float gn_read(const f16* s0, const f16* s1, int c0, int c1, size_t pix, int c) {
+    return (float)((c < c0) ? s0[pix * c0 + c] : s1[pix * c1 + (c - c0)]);
+}
+
+template <int CPT>
+__global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
+                                                         int c0, int c1, int hw, int cpg, int rows_per_block,
+                                                         float* __restrict__ ws) {
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [R][cin*2]
+    const int cin = c0 + c1, nch = cin >> 3;
+    const int n = blockIdx.y;
+    const int t = threadIdx.x;
+    const int R = (CPT == 1) ? (256 / nch) : 1;
+    const int ch_base = (CPT == 1) ? (t % nch) : t;
+    const int r0 = (CPT == 1) ? (t / nch) : 0;
+    const bool active = (CPT == 1) ? (t < R * nch) : true;
+    const int p_begin = blockIdx.x * rows_per_block;
+    const int p_end = min(hw, p_begin + rows_per_block);
+    const size_t img = (size_t)n * hw;
+
+    float sum[CPT][8], sq[CPT][8], shift[CPT][8];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { sum[q][i] = 0.f; sq[q][i] = 0.f; shift[q][i] = 0.f; }
+
+    if (active) {
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const int ch = ch_base + q * 256;
+            if (ch >= nch) continue;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                int c = ch * 8 + i;
+                shift[q][i] = gn_read(s0, s1, c0, c1, img, (c / cpg) * cpg);
+            }
+        }
+        for (int pix = p_begin + r0; pix < p_end; pix += R) {
+            const size_t gp = img + pix;
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                const int ch = ch_base + q * 256;
+                if (ch >= nch) continue;
+                const int c = ch * 8;
+                const f16* ptr = (c < c0) ? (s0 + gp * c0 + c) : (s1 + gp * c1 + (c - c0));
+                f16x8 v = *reinterpret_cast<const f16x8*>(ptr);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    float d = (float)v[i] - shift[q][i];
+                    sum[q][i] += d;
+                    sq[q][i] += d * d;
+                }
+            }
+        }
+    }
+    // block reduction over the R row-threads sharing a channel chunk
+    if (CPT == 1) {
+        if (active) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                red[(r0 * cin + ch_base * 8 + i) * 2 + 0] = sum[0][i];
+                red[(r0 * cin + ch_base * 8 + i) * 2 + 1] = sq[0][i];
+            }
+        }
+        __syncthreads();
+        for (int c = t; c < cin; c += 256) {
+            float a = 0.f, b = 0.f;
+            for (int r = 0; r < R; ++r) { a += red[(r * cin + c) * 2]; b += red[(r * cin + c) * 2 + 1]; }
+            atomicAdd(ws + ((size_t)n * cin + c) * 2 + 0, a);
+            atomicAdd(ws + ((size_t)n * cin + c) * 2 + 1, b);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            const int ch = ch_base + q * 256;
+            if (ch >= nch) continue;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                atomicAdd(ws + ((size_t)n * cin + ch * 8 + i) * 2 + 0, sum[q][i]);
+                atomicAdd(ws + ((size_t)n * cin + ch * 8 + i) * 2 + 1, sq[q][i]);
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
+                                                          int c0, int c1, int hw, int groups, float eps,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          const float* __restrict__ ws, float* __restrict__ scale,
+                                                          float* __restrict__ shift) {
+    __shared__ float g_mean[128], g_rstd[128];
+    const int cin = c0 + c1, cpg = cin / groups;
+    const int n = blockIdx.x;
+    const size_t img = (size_t)n * hw;
+    for (int g = threadIdx.x; g < groups; g += blockDim.x) {
+        double a = 0.0, b = 0.0;
+        for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+            a += ws[((size_t)n * cin + c) * 2 + 0];
+            b += ws[((size_t)n * cin + c) * 2 + 1];
+        }
+        const double cnt = (double)hw * cpg;
+        const double m1 = a / cnt;
+        double var = b / cnt - m1 * m1;
+        if (var < 0.0) var = 0.0;
+        const float s = gn_read(s0, s1, c0, c1, img, g * cpg);
+        g_mean[g] = (float)(s + m1);
+        g_rstd[g] = (float)(1.0 / sqrt(var + (double)eps));
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < cin; c += blockDim.x) {
+        const int g = c / cpg;
+        const float sc = gamma[c] * g_rstd[g];
+        scale[(size_t)n * cin + c] = sc;
+        shift[(size_t)n * cin + c] = beta[c] - g_mean[g] * sc;
+    }
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// one wave per row, up to 4 chunks (32 values) per lane in registers: exact
+// two-pass mean / variance.
+template <int NCH, bool APPLY>
+__global__ void __launch_bounds__(256) ln_kernel(const f16* __restrict__ x, int m, int c, int ld, float eps,
+                                                 float* __restrict__ stats, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, f16* __restrict__ out, int out_ld) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= m) return;
+    const int nch = c >> 3;
+    const f16* xr = x + (size_t)row * ld;
+    f16x8 v[NCH];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+        const int ch = lane + q * 64;
+        if (ch < nch) {
+            v[q] = *reinterpret_cast<const f16x8*>(xr + ch * 8);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += (float)v[q][i];
+        }
+    }
+    const float mean = wave_sum(s) / (float)c;
+    float s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+        const int ch = lane + q * 64;
+        if (ch < nch) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { float d = (float)v[q][i] - mean; s2 += d * d; }
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(s2) / (float)c + eps);
+    if (!APPLY) {
+        if (lane == 0) { stats[(size_t)row * 2] = mean; stats[(size_t)row * 2 + 1] = rstd; }
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+        const int ch = lane + q * 64;
+        if (ch < nch) {
+            f16x8 o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int cc = ch * 8 + i;
+                o[i] = (f16)(((float)v[q][i] - mean) * rstd * gamma[cc] + beta[cc]);
+            }
+            *reinterpret_cast<f16x8*>(out + (size_t)row * out_ld + ch * 8) = o;
+        }
+    }
+}
+
+template <bool APPLY>
+static int ln_dispatch(const void* x, int m, int c, int ld, float eps, float* stats, const float* gamma,
+                       const float* beta, void* out, int out_ld, hipStream_t s) {
+    const int nch = c >> 3;
+    dim3 grid((m + 3) / 4);
+    if (nch <= 64)
+        hipLaunchKernelGGL((ln_kernel<1, APPLY>), grid, dim3(256), 0, s, (const f16*)x, m, c, ld, eps, stats, gamma, beta, (f16*)out, out_ld);
+    else if (nch <= 128)
+        hipLaunchKernelGGL((ln_kernel<2, APPLY>), grid, dim3(256), 0, s, (const f16*)x, m, c, ld, eps, stats, gamma, beta, (f16*)out, out_ld);
+    else if (nch <= 256)
+        hipLaunchKernelGGL((ln_kernel<4, APPLY>), grid, dim3(256), 0, s, (const f16*)x, m, c, ld, eps, stats, gamma, beta, (f16*)out, out_ld);
+    else if (nch <= 512)
+        hipLaunchKernelGGL((ln_kernel<8, APPLY>), grid, dim3(256), 0, s, (const f16*)x, m, c, ld, eps, stats, gamma, beta, (f16*)out, out_ld);
+    else
+        return C2D_E_SHAPE;
+    return check_launch();
+}
+
+}  // namespace c2d
+
+using namespace c2d;
+
+extern "C" size_t c2d_groupnorm_workspace_size(int n, int c) { return (size_t)n * c * 2 * sizeof(float); }
+
+extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups,
+                                   float eps, const float* gamma, const float* beta, float* scale, float* shift,
+                                   void* ws, void* stream) {
+    if (!src0 || !gamma || !beta || !scale || !shift || !ws) return C2D_E_ARG;
+    if (c1 > 0 && !src1) return C2D_E_ARG;
+    const int cin = c0 + c1;
+    if ((c0 & 7) || (c1 & 7) || cin <= 0 || groups <= 0 || groups > 128 || cin % groups) return C2D_E_SHAPE;
+    if (cin > 4096 || n <= 0 || hw <= 0) return C2D_E_SHAPE;
+    if (!aligned16(src0) || (src1 && !aligned16(src1))) return C2D_E_ALIGN;
+    hipStream_t s = (hipStream_t)stream;
+    hipMemsetAsync(ws, 0, c2d_groupnorm_workspace_size(n, cin), s);
+    const int nch = cin >> 3;
+    const int cpg = cin / groups;
+    // ~128 pixels per block, at least one block per image
+    const int rows_per_block = 128;
+    dim3 grid((hw + rows_per_block - 1) / rows_per_block, n);
+    if (nch <= 256) {
+        const int R = 256 / nch;
+        const size_t lds = (size_t)R * cin * 2 * sizeof(float);
+        hipLaunchKernelGGL((gn_partial_kernel<1>), grid, dim3(256), lds, s, (const f16*)src0, (const f16*)src1, c0, c1,
+                           hw, cpg, rows_per_block, (float*)ws);
+    } else {
+        hipLaunchKernelGGL((gn_partial_kernel<2>), grid, dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1,
+                           hw, cpg, rows_per_block, (float*)ws);
+    }
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(n), dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1, hw,
+                       groups, eps, gamma, beta, (const float*)ws, scale, shift);
+    return check_launch();
+}
+
+extern "C" int c2d_layernorm_stats(const void* x, int m, int c, int ld, float eps, float* stats, void* stream) {
+    if (!x || !stats) return C2D_E_ARG;
+    if ((c & 7) || (ld & 7) || c <= 0) return C2D_E_SHAPE;
+    if (!aligned16(x)) return C2D_E_ALIGN;
+    if (m <= 0) return C2D_OK;
+    return ln_dispatch<false>(x, m, c, ld, eps, stats, nullptr, nullptr, nullptr, 0, (hipStream_t)stream);
+}
+
+extern "C" int c2d_layernorm(const void* x, int m, int c, int ld, float eps, const float* gamma, const float* beta,
+                             void* out, int out_ld, void* stream) {
+    if (!x || !gamma || !beta || !out) return C2D_E_ARG;
+    if ((c & 7) || (ld & 7) || (out_ld & 7) || c <= 0) return C2D_E_SHAPE;
+    if (!aligned16(x) || !aligned16(out)) return C2D_E_ALIGN;
+    if (m <= 0) return C2D_OK;
+    return ln_dispatch<true>(x, m, c, ld, eps, nullptr, gamma, beta, out, out_ld, (hipStream_t)stream);
+}

@@ -1,0 +1,237 @@
+"""Torch-facing wrappers over the C ABI (include/c2d.h).
+
+Tensors are plain device buffers here: activations NHWC / row-major fp16,
+statistics fp32.  Every function launches on torch's current HIP stream, so
+the calls can be captured into a torch.cuda.CUDAGraph (hipGraph) as is.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from ._lib import C2D_ACT, C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_NONE, C2D_PRO_SILU, ConvDesc, check, lib, ptr, stream_ptr
+
+F16 = torch.float16
+
+
+def _require(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a device tensor (HIP path only, no CPU fallback)")
+
+
+# ----------------------------------------------------------------- packing
+def kpad_of(k: int) -> int:
+    return (k + 63) // 64 * 64
+
+
+def pack_conv_weight(w: torch.Tensor, cin_pad: int | None = None) -> tuple[torch.Tensor, int]:
+    """[cout, cin, kh, kw] -> fp16 [cout][kpad] with K ordered (ky, kx, cin)."""
+    cout, cin, kh, kw = w.shape
+    if cin_pad and cin_pad > cin:
+        w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, cin_pad - cin))
+        cin = cin_pad
+    k = kh * kw * cin
+    wp = w.permute(0, 2, 3, 1).reshape(cout, k)
+    kp = kpad_of(k)
+    if kp > k:
+        wp = torch.nn.functional.pad(wp, (0, kp - k))
+    return wp.to(F16).contiguous(), kp
+
+
+def pack_linear_weight(w: torch.Tensor) -> tuple[torch.Tensor, int]:
+    """[out, in] -> fp16 [out][kpad]."""
+    out_f, in_f = w.shape
+    kp = kpad_of(in_f)
+    wp = torch.nn.functional.pad(w, (0, kp - in_f)) if kp > in_f else w
+    return wp.to(F16).contiguous(), kp
+
+
+def geglu_interleave(w: torch.Tensor, b: torch.Tensor | None):
+    """GEGLU proj [2I, in] (rows: h then g, diffusers chunk(2, -1)) -> rows in
+    32-row blocks [h(16) | g(16)] so one MFMA column tile pair yields h*gelu(g)."""
+    two_i = w.shape[0]
+    inner = two_i // 2
+    assert inner % 16 == 0
+    idx = torch.arange(two_i).view(2, inner // 16, 16).permute(1, 0, 2).reshape(-1)
+    wi = w[idx]
+    bi = b[idx] if b is not None else None
+    return wi, bi
+
+
+# ----------------------------------------------------------------- kernels
+def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: int, bias=None, stride: int = 1,
+         up: bool = False, x2: torch.Tensor | None = None, gn=None, gn_silu: bool = False, ln=None,
+         silu_in: bool = False, act: str | None = None, temb: torch.Tensor | None = None,
+         resid: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Implicit-GEMM conv / linear (c2d_conv2d_igemm).
+
+    x: NHWC [N, H, W, C0] fp16 (or 2-D [M, C0] for a linear layer).
+    gn: (scale, shift) fp32 [N, C0+C1]; ln: (stats [M, 2], gamma, beta).
+    """
+    _require(x, "x")
+    if x.dim() == 2:
+        n, h, w = 1, 1, x.shape[0]
+        c0 = x.shape[1]
+    else:
+        n, h, w, c0 = x.shape
+    assert x.is_contiguous() and x.dtype == F16
+    c1 = 0
+    if x2 is not None:
+        assert x2.is_contiguous() and x2.dtype == F16 and x2.shape[:-1] == x.shape[:-1]
+        c1 = x2.shape[-1]
+    if ksize == 3:
+        vh, vw = (2 * h, 2 * w) if up else (h, w)
+        oh, ow = (vh + 2 - 3) // stride + 1, (vw + 2 - 3) // stride + 1
+    else:
+        oh, ow = h, w
+    out_cols = cout // 2 if act == "geglu" else cout
+    if out is None:
+        shape = (n * oh * ow, out_cols) if x.dim() == 2 else (n, oh, ow, out_cols)
+        out = torch.empty(shape, device=x.device, dtype=F16)
+    d = ConvDesc()
+    d.src0 = ptr(x); d.src1 = ptr(x2); d.c0 = c0; d.c1 = c1
+    d.n, d.h, d.w, d.oh, d.ow = n, h, w, oh, ow
+    d.ksize, d.stride, d.up = ksize, stride, int(up)
+    d.weight = ptr(weight); d.cout = cout; d.kpad = kpad
+    if gn is not None:
+        d.pro = C2D_PRO_GN; d.pro_silu = int(gn_silu); d.pro_a = ptr(gn[0]); d.pro_b = ptr(gn[1])
+    elif ln is not None:
+        d.pro = C2D_PRO_LN; d.pro_a = ptr(ln[0]); d.gamma = ptr(ln[1]); d.beta = ptr(ln[2])
+    elif silu_in:
+        d.pro = C2D_PRO_SILU
+    else:
+        d.pro = C2D_PRO_NONE
+    d.bias = ptr(bias)
+    d.act = C2D_ACT[act]
+    if temb is not None:
+        d.temb = ptr(temb); d.temb_ld = temb.stride(0)
+    if resid is not None:
+        d.resid = ptr(resid); d.resid_ld = resid.stride(-2) if resid.dim() == 2 else resid.shape[-1]
+        assert resid.stride(-1) == 1
+    d.out = ptr(out)
+    d.out_ld = out.stride(-2) if out.dim() == 2 else out.shape[-1]
+    assert out.stride(-1) == 1
+    check(lib().c2d_conv2d_igemm(ctypes.byref(d), stream_ptr()), "c2d_conv2d_igemm")
+    return out
+
+
+def group_norm_stats(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor,
+                     x2: torch.Tensor | None = None):
+    """-> (scale, shift) fp32 [N, C] folding GroupNorm(groups, eps) + affine."""
+    _require(x, "x")
+    n = x.shape[0]
+    c0 = x.shape[-1]
+    c1 = x2.shape[-1] if x2 is not None else 0
+    hw = x.numel() // (n * c0)
+    c = c0 + c1
+    scale = torch.empty((n, c), device=x.device, dtype=torch.float32)
+    shift = torch.empty_like(scale)
+    ws = torch.empty((n, c, 2), device=x.device, dtype=torch.float32)
+    rc = lib().c2d_groupnorm_stats(ptr(x), ptr(x2), c0, c1, n, hw, groups, eps, ptr(gamma), ptr(beta),
+                                   ptr(scale), ptr(shift), ptr(ws), stream_ptr())
+    check(rc, "c2d_groupnorm_stats")
+    return scale, shift
+
+
+def layer_norm_stats(x2d: torch.Tensor, eps: float) -> torch.Tensor:
+    _require(x2d, "x")
+    m, c = x2d.shape
+    st = torch.empty((m, 2), device=x2d.device, dtype=torch.float32)
+    check(lib().c2d_layernorm_stats(ptr(x2d), m, c, x2d.stride(0), eps, ptr(st), stream_ptr()), "c2d_layernorm_stats")
+    return st
+
+
+def layer_norm(x2d: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    _require(x2d, "x")
+    m, c = x2d.shape
+    if out is None:
+        out = torch.empty((m, c), device=x2d.device, dtype=F16)
+    rc = lib().c2d_layernorm(ptr(x2d), m, c, x2d.stride(0), eps, ptr(gamma), ptr(beta), ptr(out), out.stride(0),
+                             stream_ptr())
+    check(rc, "c2d_layernorm")
+    return out
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, heads: int, lq: int, lk: int,
+              d: int, scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """q/k/v: 2-D row views [batch*L, >= heads*d] (column slices allowed)."""
+    _require(q, "q")
+    if scale is None:
+        scale = 1.0 / math.sqrt(d)
+    if out is None:
+        out = torch.empty((batch * lq, heads * d), device=q.device, dtype=F16)
+    rc = lib().c2d_attention_fwd(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+                                 out.stride(0), batch, heads, lq, lk, d, float(scale), 1, stream_ptr())
+    check(rc, "c2d_attention_fwd")
+    return out
+
+
+def window_attention(qkv: torch.Tensor, row_map: torch.Tensor, n_windows: int, heads: int, d: int,
+                     bias: torch.Tensor, mask: torch.Tensor | None, out: torch.Tensor) -> torch.Tensor:
+    n_mask = mask.shape[0] if mask is not None else 0
+    rc = lib().c2d_window_attention(ptr(qkv), qkv.stride(0), ptr(row_map), n_windows, heads, d, ptr(bias), ptr(mask),
+                                    n_mask, ptr(out), out.stride(0), stream_ptr())
+    check(rc, "c2d_window_attention")
+    return out
+
+
+def htsat_mel_patches(mel: torch.Tensor, bn_scale: torch.Tensor, bn_shift: torch.Tensor) -> torch.Tensor:
+    b, t, f = mel.shape
+    assert f == 64 and mel.dtype == torch.float32 and mel.is_contiguous()
+    out = torch.empty((b * 4096, 64), device=mel.device, dtype=F16)
+    check(lib().c2d_htsat_mel_patches(ptr(mel), b, t, ptr(bn_scale), ptr(bn_shift), ptr(out), stream_ptr()),
+          "c2d_htsat_mel_patches")
+    return out
+
+
+def patch_merge_gather(x: torch.Tensor, b: int, h: int, w: int, c: int) -> torch.Tensor:
+    out = torch.empty((b * (h // 2) * (w // 2), 4 * c), device=x.device, dtype=F16)
+    check(lib().c2d_patch_merge_gather(ptr(x), b, h, w, c, ptr(out), stream_ptr()), "c2d_patch_merge_gather")
+    return out
+
+
+def row_mean(x: torch.Tensor, b: int, rows: int) -> torch.Tensor:
+    c = x.shape[1]
+    out = torch.empty((b, c), device=x.device, dtype=torch.float32)
+    check(lib().c2d_row_mean(ptr(x), b, rows, c, x.stride(0), ptr(out), stream_ptr()), "c2d_row_mean")
+    return out
+
+
+def l2_normalize_(x: torch.Tensor) -> torch.Tensor:
+    m, c = x.shape
+    check(lib().c2d_l2_normalize(ptr(x), m, c, stream_ptr()), "c2d_l2_normalize")
+    return x
+
+
+def timestep_embedding(t_table: torch.Tensor, step_index: torch.Tensor | None, n: int, dim: int) -> torch.Tensor:
+    out = torch.empty((n, dim), device=t_table.device, dtype=F16)
+    check(lib().c2d_timestep_embedding(ptr(t_table), ptr(step_index), n, dim, ptr(out), stream_ptr()),
+          "c2d_timestep_embedding")
+    return out
+
+
+def cfg_ddim_step(eps: torch.Tensor, x: torch.Tensor, guidance: float, coef: torch.Tensor, step_index: torch.Tensor,
+                  advance: bool = True) -> torch.Tensor:
+    b, c, hgt, wid = x.shape
+    rc = lib().c2d_cfg_ddim_step(ptr(eps), ptr(x), b, c, hgt * wid, float(guidance), ptr(coef), ptr(step_index),
+                                 int(advance), stream_ptr())
+    check(rc, "c2d_cfg_ddim_step")
+    return x
+
+
+def latent_to_nhwc(x: torch.Tensor, cpad: int, dup: bool) -> torch.Tensor:
+    b, c, hgt, wid = x.shape
+    out = torch.empty(((2 if dup else 1) * b, hgt, wid, cpad), device=x.device, dtype=F16)
+    check(lib().c2d_latent_to_nhwc(ptr(x), b, c, hgt * wid, cpad, int(dup), ptr(out), stream_ptr()),
+          "c2d_latent_to_nhwc")
+    return out
+
+
+def add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    if out is None:
+        out = torch.empty_like(a)
+    check(lib().c2d_add(ptr(a), ptr(b), ptr(out), a.numel(), stream_ptr()), "c2d_add")
+    return out

@@ -1,0 +1,209 @@
+/*
+ * c2d.h — C ABI of libc2d_hip.so, the MI355X (gfx950) kernels behind the
+ * audio-conditioned SD1.5 denoise step and the CLAP HTSAT audio tower.
+ *
+ * Conventions:
+ *   - Every buffer is device memory owned by the caller; the library never
+ *     allocates.  Activations are NHWC / row-major fp16, statistics fp32.
+ *   - Every entry point is stream-ordered on the hipStream_t passed in (passed
+ *     as void* so that this header needs no HIP include) and is safe to capture
+ *     into a hipGraph: no allocation, no synchronisation, no host reads.
+ *   - Return 0 on success, a negative C2D_E_* code on a shape / alignment /
+ *     argument error (nothing is launched then), C2D_E_HIP when the launch
+ *     itself failed (hipError_t from c2d_last_hip_error(), thread-local).
+ *
+ * Which reference interface each entry point replaces is cited per function
+ * (reference = youdie006/CLAP2Diffusion @ /root/reference, plus the
+ * third-party diffusers==0.23.1 / transformers ops it glues together).
+ */
+#ifndef C2D_H
+#define C2D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define C2D_OK 0
+#define C2D_E_ARG (-1)       /* null pointer / bad enum                        */
+#define C2D_E_SHAPE (-2)     /* unsupported or inconsistent shape              */
+#define C2D_E_ALIGN (-3)     /* pointer / leading dimension not 16-B aligned   */
+#define C2D_E_HIP (-4)       /* kernel launch failed, see c2d_last_hip_error() */
+
+/* prologue applied to every in-bounds A element before the MMA */
+#define C2D_PRO_NONE 0
+#define C2D_PRO_GN 1         /* y = x*scale[n][c] + shift[n][c]  (GroupNorm affine, folded) */
+#define C2D_PRO_LN 2         /* y = (x-mean[m])*rstd[m]*gamma[c] + beta[c]                  */
+#define C2D_PRO_SILU 3       /* y = silu(x)                                                 */
+
+/* activation applied after the bias in the epilogue */
+#define C2D_ACT_NONE 0
+#define C2D_ACT_GEGLU 1      /* weight rows interleaved in 16-row h/g blocks; out = h*gelu(g) */
+#define C2D_ACT_GELU 2       /* exact erf GELU */
+#define C2D_ACT_RELU 3
+#define C2D_ACT_SILU 4
+
+/*
+ * Implicit-GEMM convolution / linear layer on MFMA (v_mfma_f32_16x16x32_f16).
+ *   out[m, j] = act( sum_k A[m,k] * W[j,k] + bias[j] ) + temb[n(m), j] + resid[m, j]
+ * where A is the (virtual) im2col of the NHWC input after the prologue, with
+ * K ordered (ky, kx, cin) and W packed as [cout][kpad] (kpad = K rounded up to 64,
+ * zero filled).  Input channels may come from two sources (skip concat:
+ * channels [0,c0) from src0, [c0,c0+c1) from src1) without materialising the
+ * concatenation.  ksize 1 = linear / 1x1 conv; ksize 3 = 3x3 conv with pad 1,
+ * stride 1 or 2, optionally reading a nearest-x2-upsampled view of the input.
+ *
+ * Replaces (diffusers 0.23.1): ResnetBlock2D.norm1/2+SiLU+conv1/conv2+temb add+
+ * shortcut, Downsample2D/Upsample2D convs, conv_in/conv_out, Transformer2DModel
+ * proj_in/proj_out, Attention.to_q/k/v/to_out, GEGLU+FeedForward, TimestepEmbedding;
+ * reached from reference models/audio_attention_processor.py:115-135 (to_q/to_k/
+ * to_v/to_out) and the UNet the processor plugs into.
+ * Also transformers ClapAudioLayer / PatchMerging / ClapProjectionLayer linears
+ * (modeling_clap.py:323-478, 680-717, 905-921) via models/audio_encoder.py:171.
+ */
+typedef struct c2d_conv_desc {
+    const void* src0;        /* fp16 NHWC [n][h][w][c0]                                   */
+    const void* src1;        /* fp16 NHWC [n][h][w][c1] or NULL                           */
+    int c0, c1;              /* channels per source (c1 = 0 without a second source)      */
+    int n, h, w;             /* input batch and spatial size (source resolution)          */
+    int oh, ow;              /* output spatial size                                       */
+    int ksize;               /* 1 or 3                                                    */
+    int stride;              /* 1 or 2 (3x3 only)                                         */
+    int up;                  /* 1: conv reads nearest-x2 upsampled input (3x3, stride 1)  */
+    const void* weight;      /* fp16 [cout][kpad]                                         */
+    int cout;                /* output columns (packed rows; GEGLU: 2x the output width)  */
+    int kpad;                /* packed K, multiple of 64, >= ksize*ksize*(c0+c1)          */
+    int pro;                 /* C2D_PRO_*                                                 */
+    int pro_silu;            /* GN prologue: apply SiLU after the affine                  */
+    const float* pro_a;      /* GN: scale [n][c0+c1]   LN: (mean,rstd) [m][2]             */
+    const float* pro_b;      /* GN: shift [n][c0+c1]   LN: unused                         */
+    const float* gamma;      /* LN gamma [c]                                              */
+    const float* beta;       /* LN beta  [c]                                              */
+    const float* bias;       /* fp32 [cout] or NULL                                       */
+    int act;                 /* C2D_ACT_*                                                 */
+    const void* temb;        /* fp16 [n][temb_ld] added per (image, column) or NULL       */
+    int temb_ld;
+    const void* resid;       /* fp16 [m][resid_ld] added after the activation or NULL     */
+    int resid_ld;
+    void* out;               /* fp16 [m][out_ld]                                          */
+    int out_ld;
+} c2d_conv_desc;
+
+int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
+
+/*
+ * GroupNorm statistics folded with the affine into per-(image, channel) scale /
+ * shift tables consumed by the C2D_PRO_GN prologue:
+ *   scale[n][c] = gamma[c]*rstd[n,g(c)], shift[n][c] = beta[c] - mean[n,g(c)]*scale[n][c]
+ * Input may be a two-source channel concat (GroupNorm over the concatenation,
+ * groups may straddle the seam).  ws: fp32 workspace of
+ * c2d_groupnorm_workspace_size(n, c) bytes; it is zeroed inside (memset node).
+ * Replaces torch.nn.GroupNorm in ResnetBlock2D.norm1/norm2 (eps 1e-5) and
+ * Transformer2DModel.norm (eps 1e-6), diffusers 0.23.1.
+ */
+size_t c2d_groupnorm_workspace_size(int n, int c);
+int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, int c1, int n, int hw,
+                        int groups, float eps, const float* gamma, const float* beta,
+                        float* scale, float* shift, void* ws, void* stream);
+
+/*
+ * LayerNorm over rows of a row-major fp16 [m][c] matrix (leading dim ld).
+ * c2d_layernorm_stats writes (mean, rstd) [m][2] for the C2D_PRO_LN prologue;
+ * c2d_layernorm writes the normalised fp16 rows (out_ld) with gamma/beta.
+ * Replaces nn.LayerNorm in BasicTransformerBlock.norm1/2/3 (diffusers) and
+ * ClapAudioPatchEmbed.norm / ClapAudioLayer.layernorm_before/after /
+ * ClapAudioEncoder.norm (modeling_clap.py:233-321, 504-621, 720-902).
+ */
+int c2d_layernorm_stats(const void* x, int m, int c, int ld, float eps, float* stats, void* stream);
+int c2d_layernorm(const void* x, int m, int c, int ld, float eps, const float* gamma,
+                  const float* beta, void* out, int out_ld, void* stream);
+
+/*
+ * Flash-style attention forward, fp16 in/out, fp32 softmax, online max.
+ *   O[b, i, h*d:(h+1)*d] = softmax_j( Q_bhi . K_bhj * scale ) V_bhj
+ * Q/K/V/O are row-major token matrices with leading dims (elements); head h
+ * occupies columns [h*d, (h+1)*d) of each.  d in {40, 64, 80, 160}.
+ * lk may be any length (tail keys masked).  K/V batch index = b / kv_div
+ * (kv_div = 1 normally).
+ * Replaces the attention math of reference AudioAttnProcessor.__call__
+ * (models/audio_attention_processor.py:114-135: head_to_batch_dim,
+ * get_attention_scores, bmm, batch_to_head_dim) and AttnProcessor2_0 (attn1).
+ */
+int c2d_attention_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                      void* o, int ldo, int batch, int heads, int lq, int lk, int d,
+                      float scale, int kv_div, void* stream);
+
+/*
+ * Swin window attention of the HTSAT tower: tokens gathered through row_map
+ * (window w, token t -> row of the [B*H*W] token matrix; encodes the cyclic
+ * shift + window partition), 64-token windows, head dim 24, relative-position
+ * bias [heads][64][64] plus an optional shift mask [n_mask][64][64] indexed by
+ * window % n_mask, output scattered back through row_map.
+ * Replaces ClapAudioSelfAttention.forward + window_partition/window_reverse/
+ * torch.roll (transformers modeling_clap.py:64-100, 323-414, 558-621).
+ */
+int c2d_window_attention(const void* qkv, int ld_qkv, const int* row_map, int n_windows,
+                         int heads, int d, const float* bias, const float* mask, int n_mask,
+                         void* out, int ldo, void* stream);
+
+/*
+ * HTSAT input stage: BatchNorm2d over mel bins (eval affine), bicubic time
+ * resize 1001->1024 (align_corners), fold to 256x256 and cut 4x4 patches:
+ * out fp16 [b*4096][64] (16 used columns, zero pad).  mel fp32 [b][t][64].
+ * Replaces ClapAudioEncoder.forward:batch_norm + reshape_mel2img and the im2col
+ * of ClapAudioPatchEmbed.proj (modeling_clap.py:761-798, 814-828, 224-321).
+ */
+int c2d_htsat_mel_patches(const float* mel, int b, int t, const float* bn_scale,
+                          const float* bn_shift, void* out, void* stream);
+
+/* Swin PatchMerging gather: [b][h][w][c] -> [b][h/2*w/2][4c] in the
+ * (r0c0, r1c0, r0c1, r1c1) order of ClapAudioPatchMerging.forward (modeling_clap.py:700-717). */
+int c2d_patch_merge_gather(const void* x, int b, int h, int w, int c, void* out, void* stream);
+
+/* Row mean over groups of `rows` consecutive rows: out fp32 [b][c] = mean_r x[b*rows+r][c]
+ * (ClapAudioEncoder avgpool over the final 64 tokens, modeling_clap.py:880-896). */
+int c2d_row_mean(const void* x, int b, int rows, int c, int ld, float* out, void* stream);
+
+/* Row-wise L2 normalise fp32 [m][c] in place (F.normalize, modeling_clap.py:1533). */
+int c2d_l2_normalize(float* x, int m, int c, void* stream);
+
+/*
+ * Sinusoidal timestep embedding of diffusers get_timestep_embedding with
+ * flip_sin_to_cos=True, downscale_freq_shift=0: out fp16 [n][dim] = [cos, sin](t*f_i).
+ * t read from device memory: t_table[*step_index] (so a captured graph can be
+ * replayed across DDIM steps), broadcast to n rows.
+ */
+int c2d_timestep_embedding(const float* t_table, const int* step_index, int n, int dim,
+                           void* out, void* stream);
+
+/*
+ * Fused classifier-free guidance + DDIM (eta = 0) update, fp32 latents:
+ *   e = eps_u + g*(eps_c - eps_u); x0 = (x - sqrt(1-a_t) e)/sqrt(a_t);
+ *   x <- sqrt(a_prev) x0 + sqrt(1 - a_prev) e
+ * eps fp16 NHWC [2b][hw][4] (uncond rows first), x fp32 NCHW [b][4][hw] in place.
+ * coef fp32 [steps][2] = (a_t, a_prev) per step, read at *step_index; when
+ * advance != 0 the kernel increments *step_index after use (last block).
+ * Replaces the pipeline CFG combine + DDIMScheduler.step (diffusers 0.23.1).
+ */
+int c2d_cfg_ddim_step(const void* eps, float* x, int b, int c, int hw, float guidance,
+                      const float* coef, int* step_index, int advance, void* stream);
+
+/* NCHW fp32 [n][c][hw] -> NHWC fp16 [2*n or n][hw][cpad] (zero-padded channels), optional
+ * duplication for the CFG pair (dup=1 writes rows n..2n-1 again). */
+int c2d_latent_to_nhwc(const float* x, int n, int c, int hw, int cpad, int dup, void* out,
+                       void* stream);
+
+/* out = a + b (fp16, same shape, n elements, multiple of 8). */
+int c2d_add(const void* a, const void* b, void* out, size_t n, void* stream);
+
+/* thread-local hipError_t of the last failed launch (0 if none) */
+int c2d_last_hip_error(void);
+/* build identification string (arch + git-free version tag) */
+const char* c2d_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* C2D_H */
