@@ -1,0 +1,214 @@
+"""Attention-processor plugin API on the HIP kernels.
+
+Mirrors the reference plugin surface (models/audio_attention_processor.py):
+  AudioAttnProcessor(level, audio_dim=768, hidden_dim=768, mode="add",
+                     dropout=0.1, bottleneck_dim=64)              (:13-41)
+  processor(attn, hidden_states, encoder_hidden_states=None,
+            attention_mask=None, temb=None, scale=1.0, **cross_attention_kwargs)  (:43-52)
+  AudioProcessorManager(unet): _create_level_mapping / setup_processors /
+            get_audio_kwargs                                      (:148-267)
+registered through unet.attn_processors / unet.set_attn_processor, audio passed
+as cross_attention_kwargs={'audio': {'early'|'mid'|'late': [B, K, 768]}}.
+
+Processors are nn.Modules with the reference parameter names (audio_proj.0,
+audio_proj.3, alpha) so reference state dicts load unchanged.  Every processor
+here accepts and ignores unknown kwargs, including on attn1.
+The compute runs on libc2d_hip.so: fused-QKV / KV GEMMs, the flash attention
+kernel, the out-projection with the block residual fused into its epilogue.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+def _as_tokens(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() != 3:
+        raise ValueError("HIP attention processors take [B, L, C] hidden states")
+    return x if x.is_contiguous() else x.contiguous()
+
+
+class AttnProcessor(nn.Module):
+    """Default processor (stock diffusers AttnProcessor semantics) on HIP.
+    Self-attention uses the fused [to_q; to_k; to_v] weight of the layer."""
+
+    fuses_residual = True
+
+    def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
+                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is not used by the SD1.5 sampling path")
+        x = _as_tokens(hidden_states)
+        b, l, c = x.shape
+        x2 = x.view(b * l, c)
+        heads, d = attn.heads, attn.dim_head
+        inner = heads * d
+        if encoder_hidden_states is None:
+            qkv = ops.conv(x2, attn.w_qkv, attn.kpad_q, 3 * inner, ksize=1)
+            if scale != 1.0:
+                qkv[:, :inner].mul_(scale)
+            o = ops.attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], b, heads, l, l, d)
+        else:
+            ehs = _as_tokens(encoder_hidden_states)
+            lk = ehs.shape[1]
+            q = ops.conv(x2, attn.to_q.weight, attn.kpad_q, inner, ksize=1)
+            if scale != 1.0:
+                q.mul_(scale)
+            kv = ops.conv(ehs.reshape(-1, ehs.shape[-1]), attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1)
+            o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d)
+        out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
+                             out=None if _residual is None else _residual.reshape(b * l, c))
+        return out.view(b, l, c)
+
+
+class AudioAttnProcessor(nn.Module):
+    """Audio-injecting cross-attention processor (reference :13-145) on HIP.
+
+    mode "add" (Add-FiLM, default):  ctx' = ctx + sigmoid(alpha) * mean_K(audio_proj(audio[level]))
+    mode "concat": ctx' = cat(ctx, adaptive_avg_pool(audio_proj(audio[level]), <= 4 tokens))
+    then q = to_q(h) * scale, k, v = to_k/to_v(ctx'), softmax(q k^T / sqrt(d)) v, to_out.
+
+    Add-FiLM is evaluated by linearity without materialising ctx':
+    K|V = ctx W_kv^T + [sigmoid(alpha) * pooled] W_kv^T, the second term entering
+    the KV GEMM epilogue as a per-image row vector (the kernel's temb input).
+    """
+
+    fuses_residual = True
+
+    def __init__(self, level: str, audio_dim: int = 768, hidden_dim: int = 768, mode: str = "add",
+                 dropout: float = 0.1, bottleneck_dim: int = 64):
+        super().__init__()
+        self.level = level
+        self.mode = mode
+        self.audio_proj = nn.Sequential(
+            nn.Linear(audio_dim, bottleneck_dim), nn.GELU(), nn.Dropout(dropout), nn.Linear(bottleneck_dim, hidden_dim))
+        self.alpha = nn.Parameter(torch.zeros(1))
+        self._packed = None
+        self._packed_key = None
+
+    def _pack(self, device):
+        key = tuple((p.data_ptr(), p._version) for p in self.parameters()) + (str(device),)
+        if self._packed_key != key:
+            l1, l2 = self.audio_proj[0], self.audio_proj[3]
+            w1, k1 = ops.pack_linear_weight(l1.weight.detach().float())
+            w2, k2 = ops.pack_linear_weight(l2.weight.detach().float())
+            self._packed = dict(w1=w1.to(device), k1=k1, b1=l1.bias.detach().float().to(device).contiguous(),
+                                w2=w2.to(device), k2=k2, b2=l2.bias.detach().float().to(device).contiguous(),
+                                n1=l1.out_features, n2=l2.out_features)
+            self._packed_key = key
+        return self._packed
+
+    def project_audio(self, audio_tokens: torch.Tensor) -> torch.Tensor:
+        """audio_proj (Linear, GELU, Dropout(eval), Linear) on the GEMM kernel -> [B, K, hidden] fp16."""
+        pk = self._pack(audio_tokens.device)
+        b, k, dim = audio_tokens.shape
+        a = audio_tokens.reshape(b * k, dim).to(torch.float16).contiguous()
+        a = ops.conv(a, pk["w1"], pk["k1"], pk["n1"], ksize=1, bias=pk["b1"], act="gelu")
+        a = ops.conv(a, pk["w2"], pk["k2"], pk["n2"], ksize=1, bias=pk["b2"])
+        return a.view(b, k, pk["n2"])
+
+    def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
+                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is not used by the SD1.5 sampling path")
+        x = _as_tokens(hidden_states)
+        b, l, c = x.shape
+        heads, d = attn.heads, attn.dim_head
+        inner = heads * d
+        ehs = encoder_hidden_states
+        audio = cross_attention_kwargs.get("audio", None)
+        audio_tokens = audio[self.level] if (audio is not None and self.level in audio) else None
+        if ehs is None:  # self-attention use of the processor (reference :117-118)
+            return AttnProcessor.__call__(self, attn, hidden_states, None, None, temb, scale, _residual)
+        ehs = _as_tokens(ehs.to(torch.float16))
+        kv_bias = None
+        if audio_tokens is not None:
+            if audio_tokens.shape[0] != b:
+                if b % audio_tokens.shape[0]:
+                    raise ValueError("audio batch must divide the UNet batch")
+                audio_tokens = audio_tokens.repeat(b // audio_tokens.shape[0], 1, 1)
+            proj = self.project_audio(audio_tokens)
+            if self.mode == "add":
+                pooled = ops.row_mean(proj.view(b * proj.shape[1], -1), b, proj.shape[1])   # [B, hidden] fp32
+                gp = (torch.sigmoid(self.alpha.detach().float().to(pooled.device)) * pooled).to(torch.float16)
+                kv_bias = ops.conv(gp, attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1)           # [B, 2*inner]
+            elif self.mode == "concat":
+                if proj.shape[1] > 4:
+                    proj = F.adaptive_avg_pool1d(proj.float().transpose(1, 2), 4).transpose(1, 2).to(torch.float16)
+                ehs = torch.cat([ehs, proj.to(ehs.dtype)], dim=1).contiguous()
+        lk = ehs.shape[1]
+        q = ops.conv(x.view(b * l, c), attn.to_q.weight, attn.kpad_q, inner, ksize=1)
+        if scale != 1.0:
+            q.mul_(scale)
+        ehs4 = ehs.view(b, 1, lk, ehs.shape[-1])
+        kv = ops.conv(ehs4, attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1, temb=kv_bias).view(b * lk, 2 * inner)
+        o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d)
+        out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
+                             out=None if _residual is None else _residual.reshape(b * l, c))
+        return out.view(b, l, c)
+
+
+class AudioProcessorManager:
+    """Maps the UNet's cross-attention processors to audio levels (reference :148-267)."""
+
+    def __init__(self, unet):
+        self.unet = unet
+        self.processors = {}
+        self.level_mapping = self._create_level_mapping()
+
+    def _create_level_mapping(self) -> Dict[str, list]:
+        mapping = {"early": [], "mid": [], "late": []}
+        for name in self.unet.attn_processors.keys():
+            if "attn1" in name:
+                continue
+            if "mid_block" in name:
+                mapping["mid"].append(name)
+            elif "down_blocks.0" in name or "down_blocks.1" in name:
+                mapping["early"].append(name)
+            elif "down_blocks.2" in name or "down_blocks.3" in name:
+                mapping["late"].append(name)
+            elif "up_blocks.0" in name or "up_blocks.1" in name:
+                mapping["late"].append(name)
+            elif "up_blocks.2" in name or "up_blocks.3" in name:
+                mapping["mid"].append(name)
+            else:
+                mapping["mid"].append(name)
+        return mapping
+
+    def setup_processors(self, audio_dim: int = 768, hidden_dim: int = None, mode: str = "add",
+                         dropout: float = 0.1, verbose: bool = True):
+        if hidden_dim is None:
+            for name in self.unet.attn_processors:
+                if "attn2" in name:
+                    hidden_dim = self.unet.get_submodule(name.rsplit(".", 1)[0]).to_k.in_features
+                    break
+            if hidden_dim is None:
+                hidden_dim = 768
+        new = dict(self.unet.attn_processors)
+        for level, names in self.level_mapping.items():
+            proc = AudioAttnProcessor(level=level, audio_dim=audio_dim, hidden_dim=hidden_dim, mode=mode,
+                                      dropout=dropout)
+            for name in names:
+                new[name] = proc
+        self.unet.set_attn_processor(new)
+        self.processors = new
+        if verbose:
+            print("Setup audio processors:")
+            for lv in ("early", "mid", "late"):
+                print(f"  {lv.capitalize()} blocks: {len(self.level_mapping[lv])}")
+
+    def level_processors(self) -> Dict[str, "AudioAttnProcessor"]:
+        out = {}
+        for level, names in self.level_mapping.items():
+            if names and isinstance(self.processors.get(names[0]), AudioAttnProcessor):
+                out[level] = self.processors[names[0]]
+        return out
+
+    def get_audio_kwargs(self, routed_tokens: Dict[str, torch.Tensor]) -> Dict:
+        return {"audio": routed_tokens}

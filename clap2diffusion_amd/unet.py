@@ -1,0 +1,372 @@
+"""SD1.5 UNet2DConditionModel on the HIP kernels (NHWC fp16 activations).
+
+The module tree and attribute names follow diffusers 0.23.1 so that
+  - diffusers / SD1.5 checkpoint keys load 1:1 (load_diffusers_state_dict),
+  - processor names match ("down_blocks.0.attentions.0.transformer_blocks.0.attn2.processor"),
+    which is what the reference AudioProcessorManager keys on
+    (models/audio_attention_processor.py:168-193),
+  - unet.attn_processors / unet.set_attn_processor behave as in diffusers.
+
+Per-step structure: conv_in, 4 down blocks, mid block, 4 up
+blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
+  ResnetBlock2D   GN1 stats -> conv1 (GN1+SiLU prologue, bias+temb epilogue) ->
+                  GN2 stats -> conv2 (GN2+SiLU prologue, bias+residual epilogue);
+                  skip concat read from two sources (never materialised);
+                  all 22 time_emb_proj GEMMs batched into one (SiLU prologue).
+  Transformer2D   GN stats -> proj_in (GN prologue) -> block -> proj_out (+residual).
+  Block           LN1 -> fused QKV GEMM -> flash attn -> to_out (+residual);
+                  LN2 -> audio cross-attn processor (+residual);
+                  FF: GEGLU GEMM with the LN3 prologue -> Linear (+residual).
+  Up/Downsample   nearest-x2 gather and stride-2 folded into the conv addressing.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .layers import HConv2d, HGroupNorm, HLayerNorm, HLinear
+from .processor import AttnProcessor
+from .weights import SD15_UNET
+
+
+class Attention(nn.Module):
+    """The diffusers Attention surface a processor relies on (to_q/to_k/to_v/
+    to_out, heads, scale, spatial_norm, norm_cross, residual_connection,
+    rescale_output_factor, head_to_batch_dim, batch_to_head_dim,
+    get_attention_scores), plus packed fused weights for the HIP processors."""
+
+    def __init__(self, query_dim: int, cross_attention_dim: int | None = None, heads: int = 8,
+                 dim_head: int | None = None, out_bias: bool = True):
+        super().__init__()
+        dim_head = dim_head or query_dim // heads
+        inner = heads * dim_head
+        ctx = cross_attention_dim or query_dim
+        self.heads, self.dim_head = heads, dim_head
+        self.scale = dim_head ** -0.5
+        self.is_cross_attention = cross_attention_dim is not None
+        self.to_q = HLinear(query_dim, inner, bias=False)
+        self.to_k = HLinear(ctx, inner, bias=False)
+        self.to_v = HLinear(ctx, inner, bias=False)
+        self.to_out = nn.ModuleList([HLinear(inner, query_dim, bias=out_bias), nn.Dropout(0.0)])
+        self.spatial_norm = None
+        self.norm_cross = None
+        self.residual_connection = False
+        self.rescale_output_factor = 1.0
+        self.upcast_attention = False
+        self.upcast_softmax = False
+        self.kpad_q = self.to_q.kpad
+        self.kpad_kv = self.to_k.kpad
+        self.register_buffer("w_qkv", None if self.is_cross_attention else
+                             torch.zeros(3 * inner, self.kpad_q, dtype=torch.float16), persistent=False)
+        self.register_buffer("w_kv", torch.zeros(2 * inner, self.kpad_kv, dtype=torch.float16), persistent=False)
+        self.processor = AttnProcessor()
+
+    @torch.no_grad()
+    def finalize(self):
+        """Concatenate the packed projections (fused QKV for self-attention, KV for both)."""
+        self.w_kv.copy_(torch.cat([self.to_k.weight, self.to_v.weight], 0))
+        if self.w_qkv is not None:
+            self.w_qkv.copy_(torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight], 0))
+
+    def set_processor(self, processor) -> None:
+        self.processor = processor
+
+    def forward(self, hidden_states, encoder_hidden_states=None, attention_mask=None, **cross_attention_kwargs):
+        return self.processor(self, hidden_states, encoder_hidden_states=encoder_hidden_states,
+                              attention_mask=attention_mask, **cross_attention_kwargs)
+
+    # -- diffusers helpers used by reference-style (torch) processors ----------
+    def head_to_batch_dim(self, tensor: torch.Tensor, out_dim: int = 3) -> torch.Tensor:
+        b, l, dim = tensor.shape
+        h = self.heads
+        t = tensor.reshape(b, l, h, dim // h).permute(0, 2, 1, 3)
+        return t.reshape(b * h, l, dim // h) if out_dim == 3 else t
+
+    def batch_to_head_dim(self, tensor: torch.Tensor) -> torch.Tensor:
+        bh, l, d = tensor.shape
+        h = self.heads
+        return tensor.reshape(bh // h, h, l, d).permute(0, 2, 1, 3).reshape(bh // h, l, d * h)
+
+    def get_attention_scores(self, query, key, attention_mask=None):
+        scores = torch.baddbmm(torch.empty(query.shape[0], query.shape[1], key.shape[1], dtype=query.dtype,
+                                           device=query.device), query, key.transpose(-1, -2), beta=0,
+                               alpha=self.scale)
+        if attention_mask is not None:
+            scores = scores + attention_mask
+        return scores.softmax(dim=-1).to(query.dtype)
+
+
+class FeedForward(nn.Module):
+    """GEGLU(dim, 4 dim) -> Dropout -> Linear(4 dim, dim); net.0.proj rows packed
+    in h/g-interleaved 16-row blocks for the GEGLU epilogue."""
+
+    def __init__(self, dim: int, mult: int = 4):
+        super().__init__()
+        inner = dim * mult
+        self.net = nn.ModuleList([nn.Module(), nn.Dropout(0.0), HLinear(inner, dim)])
+        self.net[0].proj = HLinear(dim, 2 * inner)
+
+    @torch.no_grad()
+    def load_geglu(self, w, b):
+        wi, bi = ops.geglu_interleave(w.float(), b.float())
+        self.net[0].proj.load(wi, bi)
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim: int, heads: int, cross_dim: int):
+        super().__init__()
+        self.norm1 = HLayerNorm(dim)
+        self.attn1 = Attention(dim, None, heads)
+        self.norm2 = HLayerNorm(dim)
+        self.attn2 = Attention(dim, cross_dim, heads)
+        self.norm3 = HLayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+    def _attend(self, attn: Attention, x, h, ehs, kwargs):
+        if getattr(attn.processor, "fuses_residual", False):
+            return attn(x, encoder_hidden_states=ehs, _residual=h, **kwargs)
+        out = attn(x, encoder_hidden_states=ehs, **kwargs)
+        return ops.add(out.contiguous(), h)
+
+    def forward(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict) -> torch.Tensor:
+        """h: [B, L, C] fp16 (updated in place by the fused residual epilogues)."""
+        kw = cross_attention_kwargs or {}
+        h = self._attend(self.attn1, self.norm1(h), h, None, kw)
+        h = self._attend(self.attn2, self.norm2(h), h, ehs, kw)
+        b, l, c = h.shape
+        h2 = h.view(b * l, c)
+        ff1 = self.ff.net[0].proj(h2, ln=self.norm3.prologue(h2), act="geglu")
+        self.ff.net[2](ff1, resid=h2, out=h2)
+        return h
+
+
+class Transformer2DModel(nn.Module):
+    def __init__(self, c: int, heads: int, cross_dim: int, groups: int = 32):
+        super().__init__()
+        self.norm = HGroupNorm(groups, c, 1e-6)
+        self.proj_in = HConv2d(c, c, 1)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(c, heads, cross_dim)])
+        self.proj_out = HConv2d(c, c, 1)
+
+    def forward(self, x, ehs, cross_attention_kwargs):
+        n, hh, ww, c = x.shape
+        h = self.proj_in(x, gn=self.norm.stats(x), gn_silu=False)
+        t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs)
+        return self.proj_out(t.view(n, hh, ww, c), resid=x)
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin: int, cout: int, temb_ch: int = 1280, groups: int = 32, eps: float = 1e-5):
+        super().__init__()
+        self.cin, self.cout = cin, cout
+        self.norm1 = HGroupNorm(groups, cin, eps)
+        self.conv1 = HConv2d(cin, cout, 3)
+        self.time_emb_proj = HLinear(temb_ch, cout) if temb_ch else None
+        self.norm2 = HGroupNorm(groups, cout, eps)
+        self.dropout = nn.Dropout(0.0)
+        self.conv2 = HConv2d(cout, cout, 3)
+        self.conv_shortcut = HConv2d(cin, cout, 1) if cin != cout else None
+        self.temb_off = None  # column offset into the batched time_emb_proj output
+
+    def forward(self, x, temb_all=None, skip=None):
+        sc1 = self.norm1.stats(x, skip)
+        temb = None
+        if temb_all is not None:
+            temb = temb_all[:, self.temb_off:self.temb_off + self.cout]
+        h = self.conv1(x, x2=skip, gn=sc1, gn_silu=True, temb=temb)
+        sc2 = self.norm2.stats(h)
+        res = self.conv_shortcut(x, x2=skip) if self.conv_shortcut is not None else x
+        return self.conv2(h, gn=sc2, gn_silu=True, resid=res)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = HConv2d(c, c, 3, stride=2)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = HConv2d(c, c, 3)
+
+    def forward(self, x):
+        return self.conv(x, up=True)
+
+
+class _Block(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.resnets = nn.ModuleList()
+        self.attentions = nn.ModuleList()
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, cin: int, dim: int):
+        super().__init__()
+        self.linear_1 = HLinear(cin, dim)
+        self.linear_2 = HLinear(dim, dim)
+
+    def forward(self, t_sin):
+        return self.linear_2(self.linear_1(t_sin, act="silu"))
+
+
+class UNetOutput:
+    def __init__(self, sample):
+        self.sample = sample
+
+    def __getitem__(self, i):
+        return (self.sample,)[i]
+
+
+class UNet2DConditionModel(nn.Module):
+    def __init__(self, cfg: dict = SD15_UNET):
+        super().__init__()
+        self.cfg = dict(cfg)
+        ch = cfg["block_out_channels"]
+        heads, ctx, groups = cfg["heads"], cfg["cross_attention_dim"], cfg["norm_groups"]
+        temb_ch = ch[0] * 4
+        self.in_pad = 8
+        self.conv_in = HConv2d(cfg["in_channels"], ch[0], 3, cin_pad=self.in_pad)
+        self.time_embedding = TimestepEmbedding(ch[0], temb_ch)
+        self.down_blocks = nn.ModuleList()
+        out_c = ch[0]
+        for i, c in enumerate(ch):
+            blk = _Block()
+            in_c, out_c = out_c, c
+            for j in range(cfg["layers_per_block"]):
+                blk.resnets.append(ResnetBlock2D(in_c if j == 0 else out_c, out_c, temb_ch, groups))
+                if cfg["attn_blocks"][i]:
+                    blk.attentions.append(Transformer2DModel(out_c, heads, ctx, groups))
+            if i < len(ch) - 1:
+                blk.downsamplers = nn.ModuleList([Downsample2D(out_c)])
+            self.down_blocks.append(blk)
+        self.mid_block = _Block()
+        self.mid_block.resnets.append(ResnetBlock2D(ch[-1], ch[-1], temb_ch, groups))
+        self.mid_block.attentions.append(Transformer2DModel(ch[-1], heads, ctx, groups))
+        self.mid_block.resnets.append(ResnetBlock2D(ch[-1], ch[-1], temb_ch, groups))
+        self.up_blocks = nn.ModuleList()
+        rev = list(reversed(ch))
+        rev_attn = list(reversed(cfg["attn_blocks"]))
+        out_c = rev[0]
+        n_up = cfg["layers_per_block"] + 1
+        for i in range(len(rev)):
+            blk = _Block()
+            prev_c, out_c = out_c, rev[i]
+            in_c = rev[min(i + 1, len(rev) - 1)]
+            for j in range(n_up):
+                skip = in_c if j == n_up - 1 else out_c
+                r_in = prev_c if j == 0 else out_c
+                blk.resnets.append(ResnetBlock2D(r_in + skip, out_c, temb_ch, groups))
+                blk.resnets[-1].skip_ch = skip
+                if rev_attn[i]:
+                    blk.attentions.append(Transformer2DModel(out_c, heads, ctx, groups))
+            if i < len(rev) - 1:
+                blk.upsamplers = nn.ModuleList([Upsample2D(out_c)])
+            self.up_blocks.append(blk)
+        self.conv_norm_out = HGroupNorm(groups, ch[0], cfg["norm_eps"])
+        self.conv_out = HConv2d(ch[0], cfg["out_channels"], 3)
+        resnets = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+        off = 0
+        for r in resnets:
+            r.temb_off = off
+            off += r.cout
+        self.temb_total = off
+        kp = ops.kpad_of(temb_ch)
+        self.register_buffer("w_temb_all", torch.zeros(off, kp, dtype=torch.float16), persistent=False)
+        self.register_buffer("b_temb_all", torch.zeros(off, dtype=torch.float32), persistent=False)
+        self.temb_kpad = kp
+
+    # ------------------------------------------------------------ weights
+    @torch.no_grad()
+    def load_diffusers_state_dict(self, sd: dict) -> None:
+        """Load diffusers-0.23.1 UNet2DConditionModel keys (SD1.5 layout)."""
+        used = set()
+        for name, m in self.named_modules():
+            if isinstance(m, FeedForward):
+                k = name + ".net.0.proj"
+                m.load_geglu(sd[k + ".weight"], sd[k + ".bias"])
+                used |= {k + ".weight", k + ".bias"}
+        for name, m in self.named_modules():
+            if isinstance(m, (HLinear, HConv2d, HGroupNorm, HLayerNorm)):
+                if name.endswith("net.0.proj"):
+                    continue
+                wk, bk = name + ".weight", name + ".bias"
+                m.load(sd[wk], sd.get(bk))
+                used |= {wk, bk}
+        missing = [k for k in sd if k not in used]
+        if missing:
+            raise KeyError(f"unused checkpoint keys: {missing[:5]} ...")
+        self.finalize()
+
+    @torch.no_grad()
+    def finalize(self) -> None:
+        for m in self.modules():
+            if isinstance(m, Attention):
+                m.finalize()
+        rs = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+        self.w_temb_all.copy_(torch.cat([r.time_emb_proj.weight for r in rs], 0))
+        self.b_temb_all.copy_(torch.cat([r.time_emb_proj.bias for r in rs], 0))
+
+    # ------------------------------------------------------------ processors
+    @property
+    def attn_processors(self) -> dict:
+        return {f"{n}.processor": m.processor for n, m in self.named_modules() if isinstance(m, Attention)}
+
+    def set_attn_processor(self, processor) -> None:
+        for n, m in self.named_modules():
+            if isinstance(m, Attention):
+                m.set_processor(processor[f"{n}.processor"] if isinstance(processor, dict) else processor)
+
+    # ------------------------------------------------------------ forward
+    def forward_nhwc(self, x: torch.Tensor, t_sin: torch.Tensor, ehs: torch.Tensor,
+                     cross_attention_kwargs: dict | None = None) -> torch.Tensor:
+        """x: [N, H, W, 8] fp16 (latent zero-padded to 8 ch); t_sin: [N, 320] fp16
+        sinusoidal embedding; ehs: [N, 77, 768] fp16. Returns eps [N, H, W, 4] fp16."""
+        kw = cross_attention_kwargs or {}
+        temb = self.time_embedding(t_sin)
+        temb_all = ops.conv(temb, self.w_temb_all, self.temb_kpad, self.temb_total, ksize=1, bias=self.b_temb_all,
+                            silu_in=True)
+        h = self.conv_in(x)
+        skips = [h]
+        for blk in self.down_blocks:
+            for j, r in enumerate(blk.resnets):
+                h = r(h, temb_all)
+                if len(blk.attentions):
+                    h = blk.attentions[j](h, ehs, kw)
+                skips.append(h)
+            if hasattr(blk, "downsamplers"):
+                h = blk.downsamplers[0](h)
+                skips.append(h)
+        mb = self.mid_block
+        h = mb.resnets[0](h, temb_all)
+        h = mb.attentions[0](h, ehs, kw)
+        h = mb.resnets[1](h, temb_all)
+        for blk in self.up_blocks:
+            for j, r in enumerate(blk.resnets):
+                h = r(h, temb_all, skip=skips.pop())
+                if len(blk.attentions):
+                    h = blk.attentions[j](h, ehs, kw)
+            if hasattr(blk, "upsamplers"):
+                h = blk.upsamplers[0](h)
+        return self.conv_out(h, gn=self.conv_norm_out.stats(h), gn_silu=True)
+
+    def forward(self, sample: torch.Tensor, timestep, encoder_hidden_states: torch.Tensor,
+                cross_attention_kwargs: dict | None = None, return_dict: bool = True):
+        """diffusers-compatible entry: sample [N, 4, H, W] -> eps [N, 4, H, W] fp16."""
+        n = sample.shape[0]
+        x = ops.latent_to_nhwc(sample.float().contiguous(), self.in_pad, dup=False)
+        t = torch.as_tensor(timestep, dtype=torch.float32, device=sample.device).reshape(-1)
+        if t.numel() == 1:
+            t_sin = ops.timestep_embedding(t.contiguous(), None, n, self.cfg["block_out_channels"][0])
+        else:  # per-sample timesteps: one row at a time through the same kernel
+            t_sin = torch.cat([ops.timestep_embedding(t[i:i + 1].contiguous(), None, 1,
+                                                      self.cfg["block_out_channels"][0]) for i in range(n)])
+        ehs = encoder_hidden_states.to(torch.float16).contiguous()
+        eps = self.forward_nhwc(x, t_sin, ehs, cross_attention_kwargs)
+        out = eps.permute(0, 3, 1, 2).contiguous()
+        return UNetOutput(out) if return_dict else (out,)

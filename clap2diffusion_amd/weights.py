@@ -1,0 +1,215 @@
+"""Deterministic synthetic weights in the checkpoint key
+layouts the reference stack loads: diffusers-0.23.1 UNet2DConditionModel /
+AutoencoderKL keys for SD1.5, transformers ClapModel keys for HTSAT.
+
+No network and no checkpoints exist here, so every weight is drawn from a
+per-tensor seeded generator (seed = f(base_seed, crc32(key))): the same key
+gives the same tensor on every rank and in every process.  Scales are chosen
+to keep activations O(1) through 50 DDIM steps; norm affines are non-trivial
+(gamma ~ 1 + 0.1 N(0,1), beta ~ 0.1 N(0,1)) so the parity tests exercise them.
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from collections import OrderedDict
+
+import torch
+
+SD15_UNET = dict(
+    in_channels=4, out_channels=4, block_out_channels=(320, 640, 1280, 1280), layers_per_block=2,
+    cross_attention_dim=768, heads=8, norm_groups=32, norm_eps=1e-5, attn_blocks=(True, True, True, False),
+)
+
+SD15_VAE = dict(latent_channels=4, block_out_channels=(128, 256, 512, 512), layers_per_block=2, norm_groups=32,
+                out_channels=3)
+
+
+def unet_param_shapes(cfg: dict = SD15_UNET) -> "OrderedDict[str, tuple]":
+    """diffusers UNet2DConditionModel state-dict keys -> shapes (SD1.5 topology)."""
+    S: "OrderedDict[str, tuple]" = OrderedDict()
+    ch = cfg["block_out_channels"]
+    ctx = cfg["cross_attention_dim"]
+    temb = ch[0] * 4
+
+    def lin(p, i, o, bias=True):
+        S[p + ".weight"] = (o, i)
+        if bias:
+            S[p + ".bias"] = (o,)
+
+    def conv(p, i, o, k):
+        S[p + ".weight"] = (o, i, k, k)
+        S[p + ".bias"] = (o,)
+
+    def norm(p, c):
+        S[p + ".weight"] = (c,)
+        S[p + ".bias"] = (c,)
+
+    def resnet(p, i, o):
+        norm(p + ".norm1", i)
+        conv(p + ".conv1", i, o, 3)
+        lin(p + ".time_emb_proj", temb, o)
+        norm(p + ".norm2", o)
+        conv(p + ".conv2", o, o, 3)
+        if i != o:
+            conv(p + ".conv_shortcut", i, o, 1)
+
+    def transformer(p, c):
+        norm(p + ".norm", c)
+        conv(p + ".proj_in", c, c, 1)
+        b = p + ".transformer_blocks.0"
+        norm(b + ".norm1", c)
+        for n in ("to_q", "to_k", "to_v"):
+            lin(f"{b}.attn1.{n}", c, c, bias=False)
+        lin(b + ".attn1.to_out.0", c, c)
+        norm(b + ".norm2", c)
+        lin(b + ".attn2.to_q", c, c, bias=False)
+        lin(b + ".attn2.to_k", ctx, c, bias=False)
+        lin(b + ".attn2.to_v", ctx, c, bias=False)
+        lin(b + ".attn2.to_out.0", c, c)
+        norm(b + ".norm3", c)
+        lin(b + ".ff.net.0.proj", c, 8 * c)
+        lin(b + ".ff.net.2", 4 * c, c)
+        conv(p + ".proj_out", c, c, 1)
+
+    lin("time_embedding.linear_1", ch[0], temb)
+    lin("time_embedding.linear_2", temb, temb)
+    conv("conv_in", cfg["in_channels"], ch[0], 3)
+    out_c = ch[0]
+    for i, c in enumerate(ch):
+        in_c, out_c = out_c, c
+        for j in range(cfg["layers_per_block"]):
+            resnet(f"down_blocks.{i}.resnets.{j}", in_c if j == 0 else out_c, out_c)
+            if cfg["attn_blocks"][i]:
+                transformer(f"down_blocks.{i}.attentions.{j}", out_c)
+        if i < len(ch) - 1:
+            conv(f"down_blocks.{i}.downsamplers.0.conv", out_c, out_c, 3)
+    resnet("mid_block.resnets.0", ch[-1], ch[-1])
+    transformer("mid_block.attentions.0", ch[-1])
+    resnet("mid_block.resnets.1", ch[-1], ch[-1])
+    rev = list(reversed(ch))
+    rev_attn = list(reversed(cfg["attn_blocks"]))
+    out_c = rev[0]
+    for i in range(len(rev)):
+        prev_c, out_c = out_c, rev[i]
+        in_c = rev[min(i + 1, len(rev) - 1)]
+        n = cfg["layers_per_block"] + 1
+        for j in range(n):
+            skip = in_c if j == n - 1 else out_c
+            r_in = prev_c if j == 0 else out_c
+            resnet(f"up_blocks.{i}.resnets.{j}", r_in + skip, out_c)
+            if rev_attn[i]:
+                transformer(f"up_blocks.{i}.attentions.{j}", out_c)
+        if i < len(rev) - 1:
+            conv(f"up_blocks.{i}.upsamplers.0.conv", out_c, out_c, 3)
+    norm("conv_norm_out", ch[0])
+    conv("conv_out", ch[0], cfg["out_channels"], 3)
+    return S
+
+
+def vae_decoder_param_shapes(cfg: dict = SD15_VAE) -> "OrderedDict[str, tuple]":
+    """diffusers AutoencoderKL decoder + post_quant_conv keys (SD1.5 topology)."""
+    S: "OrderedDict[str, tuple]" = OrderedDict()
+    ch = list(reversed(cfg["block_out_channels"]))
+
+    def conv(p, i, o, k):
+        S[p + ".weight"] = (o, i, k, k)
+        S[p + ".bias"] = (o,)
+
+    def norm(p, c):
+        S[p + ".weight"] = (c,)
+        S[p + ".bias"] = (c,)
+
+    def resnet(p, i, o):
+        norm(p + ".norm1", i)
+        conv(p + ".conv1", i, o, 3)
+        norm(p + ".norm2", o)
+        conv(p + ".conv2", o, o, 3)
+        if i != o:
+            conv(p + ".conv_shortcut", i, o, 1)
+
+    lc = cfg["latent_channels"]
+    conv("post_quant_conv", lc, lc, 1)
+    conv("decoder.conv_in", lc, ch[0], 3)
+    resnet("decoder.mid_block.resnets.0", ch[0], ch[0])
+    a = "decoder.mid_block.attentions.0"
+    norm(a + ".group_norm", ch[0])
+    for n in ("to_q", "to_k", "to_v", "to_out.0"):
+        S[f"{a}.{n}.weight"] = (ch[0], ch[0])
+        S[f"{a}.{n}.bias"] = (ch[0],)
+    resnet("decoder.mid_block.resnets.1", ch[0], ch[0])
+    out_c = ch[0]
+    for i, c in enumerate(ch):
+        prev, out_c = out_c, c
+        for j in range(cfg["layers_per_block"] + 1):
+            resnet(f"decoder.up_blocks.{i}.resnets.{j}", prev if j == 0 else out_c, out_c)
+        if i < len(ch) - 1:
+            conv(f"decoder.up_blocks.{i}.upsamplers.0.conv", out_c, out_c, 3)
+    norm("decoder.conv_norm_out", ch[-1])
+    conv("decoder.conv_out", ch[-1], cfg["out_channels"], 3)
+    return S
+
+
+def key_seed(base: int, key: str) -> int:
+    return (base * 1000003 + zlib.crc32(key.encode())) % (2 ** 31 - 1)
+
+
+def _init_one(key: str, shape: tuple, gen: torch.Generator, device) -> torch.Tensor:
+    leaf = key.rsplit(".", 2)
+    is_norm = any(s in key for s in ("norm", "group_norm")) and len(shape) == 1
+    if is_norm and key.endswith(".weight"):
+        return 1.0 + 0.1 * torch.randn(shape, generator=gen, device=device)
+    if key.endswith(".bias"):
+        return 0.02 * torch.randn(shape, generator=gen, device=device) if not is_norm else \
+            0.1 * torch.randn(shape, generator=gen, device=device)
+    if len(shape) == 4:  # conv: torch-default-like scale 1/sqrt(3 fan_in)
+        fan_in = shape[1] * shape[2] * shape[3]
+        std = 1.0 / math.sqrt(3.0 * fan_in)
+        if key.startswith("conv_out") or key.endswith("decoder.conv_out.weight"):
+            std *= 0.5
+        return std * torch.randn(shape, generator=gen, device=device)
+    if len(shape) == 2:  # linear: N(0, 0.02^2), attention/ff projections
+        del leaf
+        return 0.02 * torch.randn(shape, generator=gen, device=device)
+    return torch.randn(shape, generator=gen, device=device)
+
+
+def synth_state_dict(shapes: "OrderedDict[str, tuple]", seed: int = 0, device="cpu",
+                     dtype=torch.float32) -> "OrderedDict[str, torch.Tensor]":
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    gen = torch.Generator(device=device)
+    for k, shp in shapes.items():
+        gen.manual_seed(key_seed(seed, k))
+        sd[k] = _init_one(k, shp, gen, device).to(dtype)
+    return sd
+
+
+def synth_unet(seed: int = 0, device="cpu", dtype=torch.float32, cfg: dict = SD15_UNET):
+    return synth_state_dict(unet_param_shapes(cfg), seed, device, dtype)
+
+
+def synth_vae_decoder(seed: int = 0, device="cpu", dtype=torch.float32, cfg: dict = SD15_VAE):
+    return synth_state_dict(vae_decoder_param_shapes(cfg), seed + 17, device, dtype)
+
+
+def synth_processor_weights(level: str, seed: int = 0, audio_dim: int = 768, hidden_dim: int = 768,
+                            bottleneck: int = 64) -> "OrderedDict[str, torch.Tensor]":
+    """AudioAttnProcessor state dict (reference models/audio_attention_processor.py:33-41):
+    audio_proj.0 Linear(audio_dim, 64), audio_proj.3 Linear(64, hidden_dim), alpha [1]."""
+    shapes = OrderedDict([
+        ("audio_proj.0.weight", (bottleneck, audio_dim)), ("audio_proj.0.bias", (bottleneck,)),
+        ("audio_proj.3.weight", (hidden_dim, bottleneck)), ("audio_proj.3.bias", (hidden_dim,)),
+    ])
+    sd = OrderedDict()
+    g = torch.Generator()
+    for k, s in shapes.items():
+        g.manual_seed(key_seed(seed, f"proc.{level}.{k}"))
+        fan_in = s[1] if len(s) == 2 else s[0]
+        sd[k] = torch.randn(s, generator=g) / math.sqrt(fan_in)
+    g.manual_seed(key_seed(seed, f"proc.{level}.alpha"))
+    sd["alpha"] = torch.randn(1, generator=g)
+    return sd
+
+
+def param_count(shapes) -> int:
+    return sum(math.prod(s) for s in shapes.values())
