@@ -213,3 +213,88 @@ def synth_processor_weights(level: str, seed: int = 0, audio_dim: int = 768, hid
 
 def param_count(shapes) -> int:
     return sum(math.prod(s) for s in shapes.values())
+
+
+# ------------------------------------------------------------------ HTSAT / generic
+HTSAT_CFG = dict(depths=(2, 2, 6, 2), embed=96, heads=(4, 8, 16, 32), window=8, mlp_ratio=4, mel_bins=64,
+                 hidden=768, proj_dim=512)
+
+
+def htsat_param_shapes(cfg: dict = HTSAT_CFG) -> "OrderedDict[str, tuple]":
+    """transformers ClapModel audio keys (htsat-unfused, enable_fusion False):
+    audio_model.audio_encoder.* and audio_projection.* (modeling_clap.py:720-921)."""
+    S: "OrderedDict[str, tuple]" = OrderedDict()
+    e = "audio_model.audio_encoder."
+    S[e + "patch_embed.proj.weight"] = (cfg["embed"], 1, 4, 4)
+    S[e + "patch_embed.proj.bias"] = (cfg["embed"],)
+    S[e + "patch_embed.norm.weight"] = (cfg["embed"],)
+    S[e + "patch_embed.norm.bias"] = (cfg["embed"],)
+    w = cfg["window"]
+    for i, depth in enumerate(cfg["depths"]):
+        dim = cfg["embed"] * 2 ** i
+        for j in range(depth):
+            b = f"{e}layers.{i}.blocks.{j}."
+            S[b + "layernorm_before.weight"] = (dim,)
+            S[b + "layernorm_before.bias"] = (dim,)
+            S[b + "attention.self.relative_position_bias_table"] = ((2 * w - 1) ** 2, cfg["heads"][i])
+            for n in ("query", "key", "value"):
+                S[f"{b}attention.self.{n}.weight"] = (dim, dim)
+                S[f"{b}attention.self.{n}.bias"] = (dim,)
+            S[b + "attention.output.dense.weight"] = (dim, dim)
+            S[b + "attention.output.dense.bias"] = (dim,)
+            S[b + "layernorm_after.weight"] = (dim,)
+            S[b + "layernorm_after.bias"] = (dim,)
+            S[b + "intermediate.dense.weight"] = (cfg["mlp_ratio"] * dim, dim)
+            S[b + "intermediate.dense.bias"] = (cfg["mlp_ratio"] * dim,)
+            S[b + "output.dense.weight"] = (dim, cfg["mlp_ratio"] * dim)
+            S[b + "output.dense.bias"] = (dim,)
+        if i < len(cfg["depths"]) - 1:
+            S[f"{e}layers.{i}.downsample.reduction.weight"] = (2 * dim, 4 * dim)
+            S[f"{e}layers.{i}.downsample.norm.weight"] = (4 * dim,)
+            S[f"{e}layers.{i}.downsample.norm.bias"] = (4 * dim,)
+    for n in ("weight", "bias", "running_mean", "running_var"):
+        S[f"{e}batch_norm.{n}"] = (cfg["mel_bins"],)
+    S[e + "norm.weight"] = (cfg["hidden"],)
+    S[e + "norm.bias"] = (cfg["hidden"],)
+    S["audio_projection.linear1.weight"] = (cfg["proj_dim"], cfg["hidden"])
+    S["audio_projection.linear1.bias"] = (cfg["proj_dim"],)
+    S["audio_projection.linear2.weight"] = (cfg["proj_dim"], cfg["proj_dim"])
+    S["audio_projection.linear2.bias"] = (cfg["proj_dim"],)
+    return S
+
+
+def synth_generic(shapes, seed: int = 0, tag: str = "", device="cpu") -> "OrderedDict[str, torch.Tensor]":
+    """Name-pattern synthetic init for small modules (HTSAT, projectors)."""
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    g = torch.Generator(device=device)
+    for k, s in shapes.items():
+        s = tuple(s)
+        g.manual_seed(key_seed(seed, tag + k))
+        r = torch.randn(s, generator=g, device=device) if len(s) else torch.randn((), generator=g, device=device)
+        leaf = k.rsplit(".", 1)[-1]
+        normish = any(t in k for t in ("norm", "ln_", "layer_norms", "batch_norm")) or k.endswith("ffn.0.weight") \
+            or k.endswith("ffn.0.bias") or k.endswith("shared_mlp.2.weight") or k.endswith("shared_mlp.2.bias") \
+            or k.endswith("weight_network.2.weight") or k.endswith("weight_network.2.bias") \
+            or k.endswith("output_proj.1.weight") or k.endswith("output_proj.1.bias")
+        if leaf == "running_var":
+            v = 0.5 + r.abs()
+        elif leaf == "running_mean":
+            v = 0.1 * r
+        elif len(s) == 1 and normish and leaf == "weight":
+            v = 1.0 + 0.1 * r
+        elif len(s) == 1 and normish and leaf == "bias":
+            v = 0.1 * r
+        elif leaf in ("bias", "in_proj_bias"):
+            v = 0.02 * r
+        elif "relative_position_bias_table" in k:
+            v = 0.5 * r
+        elif len(s) >= 2 and (leaf in ("weight", "in_proj_weight")):
+            v = r / math.sqrt(math.prod(s[1:]))
+        else:
+            v = 0.1 * r
+        sd[k] = v
+    return sd
+
+
+def synth_htsat(seed: int = 0, device="cpu") -> "OrderedDict[str, torch.Tensor]":
+    return synth_generic(htsat_param_shapes(), seed, "htsat.", device)

@@ -1,0 +1,59 @@
+"""HIP path against the golden vectors of the reference's own code:
+AudioAttnProcessor (HIP) vs the reference processor, HTSATEncoder (HIP) vs
+transformers ClapModel.  fp16 storage / fp32 accumulate; tolerances stated per test."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from clap2diffusion_amd.htsat import HTSATEncoder
+from clap2diffusion_amd.processor import AudioAttnProcessor
+from clap2diffusion_amd.unet import Attention
+from clap2diffusion_amd.weights import synth_htsat, synth_processor_weights
+from tests.test_golden_cpu import mini_attention_weights
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm()).item(), ((a - b).abs().max() / b.abs().max()).item()
+
+
+@pytest.mark.parametrize("c,l", [(320, 48), (640, 32), (1280, 16), (1280, 8)])
+@pytest.mark.parametrize("mode", ["add", "concat"])
+def test_hip_processor_matches_reference(dev, c, l, mode):
+    gd = np.load(G / "processor.npz")
+    ci = [(320, 48), (640, 32), (1280, 16), (1280, 8)].index((c, l))
+    w, _ = mini_attention_weights(c, 100 + ci)
+    attn = Attention(c, 768, heads=8).to(dev)
+    attn.to_q.load(w["to_q.weight"])
+    attn.to_k.load(w["to_k.weight"])
+    attn.to_v.load(w["to_v.weight"])
+    attn.to_out[0].load(w["to_out.0.weight"], w["to_out.0.bias"])
+    attn.finalize()
+    proc = AudioAttnProcessor(level="mid", mode=mode)
+    proc.load_state_dict(synth_processor_weights("mid", seed=ci))
+    proc = proc.to(dev).eval()
+    h = torch.from_numpy(gd[f"c{c}_l{l}_h"]).to(dev).half()
+    ehs = torch.from_numpy(gd["ehs"]).to(dev).half()
+    audio = torch.from_numpy(gd["audio"]).to(dev)
+    with torch.no_grad():
+        out = proc(attn, h, encoder_hidden_states=ehs, audio={"mid": audio})
+    l2, mx = rel(out, torch.from_numpy(gd[f"c{c}_l{l}_{mode}_out"]))
+    assert l2 <= 5e-3 and mx <= 2e-2, (l2, mx)
+
+
+def test_hip_htsat_matches_transformers(dev):
+    gd = np.load(G / "htsat.npz")
+    enc = HTSATEncoder().to(dev)
+    enc.load_clap_state_dict(synth_htsat(0))
+    mel = torch.from_numpy(gd["mel"]).to(dev)
+    emb = enc(mel)
+    ref = torch.from_numpy(gd["embedding"])
+    l2, mx = rel(emb, ref)
+    cos = torch.nn.functional.cosine_similarity(emb.cpu(), ref, dim=-1)
+    # fp16 residual stream through 12 Swin blocks: rel-L2 <= 1e-2, cosine >= 0.9999
+    assert l2 <= 1e-2 and cos.min().item() >= 0.9999, (l2, mx, cos)
