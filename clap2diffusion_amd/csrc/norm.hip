@@ -1,14 +1,17 @@
 // GroupNorm statistics (folded into per-(image, channel) affine tables) and
 // LayerNorm statistics / apply for gfx950.  All HBM-bound: 16-B vector loads,
-// per-block LDS reduction, one fp32 atomic per (block, channel, moment).
+// per-block LDS reduction, per-block partials reduced by a second kernel.
 #include "common.h"
 
 namespace c2d {
 
 // ---------------------------------------------------------------- GroupNorm
-// ws layout: fp32 [n][cin][2] shifted moments (sum(x-s_g), sum((x-s_g)^2)).
-// The per-group shift s_g = x[n, pixel 0, first channel of g] keeps the
-// one-pass variance well conditioned when |mean| >> std.
+// ws layout: fp32 [n][nblk][cin][2] per-block shifted moments
+// (sum(x-s_g), sum((x-s_g)^2)), written with plain stores and reduced in a
+// fixed order by the finalize kernel: no atomics, no memset, bitwise
+// reproducible, graph-replay safe.  The per-group shift
+// s_g = x[n, pixel 0, first channel of g] keeps the one-pass variance well
+// conditioned when |mean| >> std.
 __device__ __forceinline__ float gn_read(const f16* s0, const f16* s1, int c0, int c1, size_t pix, int c) {
     return (float)((c < c0) ? s0[pix * c0 + c] : s1[pix * c1 + (c - c0)]);
 }
@@ -74,28 +77,27 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
             }
         }
         __syncthreads();
+        float* dst = ws + (((size_t)n * gridDim.x + blockIdx.x) * cin) * 2;
         for (int c = t; c < cin; c += 256) {
             float a = 0.f, b = 0.f;
             for (int r = 0; r < R; ++r) { a += red[(r * cin + c) * 2]; b += red[(r * cin + c) * 2 + 1]; }
-            atomicAdd(ws + ((size_t)n * cin + c) * 2 + 0, a);
-            atomicAdd(ws + ((size_t)n * cin + c) * 2 + 1, b);
+            dst[c * 2 + 0] = a;
+            dst[c * 2 + 1] = b;
         }
     } else {
 #pragma unroll
         for (int q = 0; q < CPT; ++q) {
             const int ch = ch_base + q * 256;
             if (ch >= nch) continue;
+            float* dst = ws + (((size_t)n * gridDim.x + blockIdx.x) * cin + ch * 8) * 2;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                atomicAdd(ws + ((size_t)n * cin + ch * 8 + i) * 2 + 0, sum[q][i]);
-                atomicAdd(ws + ((size_t)n * cin + ch * 8 + i) * 2 + 1, sq[q][i]);
-            }
+            for (int i = 0; i < 8; ++i) { dst[i * 2] = sum[q][i]; dst[i * 2 + 1] = sq[q][i]; }
         }
     }
 }
 
 __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
-                                                          int c0, int c1, int hw, int groups, float eps,
+                                                          int c0, int c1, int hw, int groups, int nblk, float eps,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           const float* __restrict__ ws, float* __restrict__ scale,
                                                           float* __restrict__ shift) {
@@ -103,12 +105,23 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict_
     const int cin = c0 + c1, cpg = cin / groups;
     const int n = blockIdx.x;
     const size_t img = (size_t)n * hw;
-    for (int g = threadIdx.x; g < groups; g += blockDim.x) {
-        double a = 0.0, b = 0.0;
-        for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-            a += ws[((size_t)n * cin + c) * 2 + 0];
-            b += ws[((size_t)n * cin + c) * 2 + 1];
+    const int lpg = 256 / groups;               // lanes per group (power of two, <= 64)
+    const int g = threadIdx.x / lpg, sub = threadIdx.x - g * lpg;
+    double a = 0.0, b = 0.0;
+    if (g < groups) {
+        const int items = nblk * cpg;
+        for (int it = sub; it < items; it += lpg) {
+            const int blk = it / cpg, c = g * cpg + (it - blk * cpg);
+            const float* p = ws + (((size_t)n * nblk + blk) * cin + c) * 2;
+            a += p[0];
+            b += p[1];
         }
+    }
+    for (int o = lpg >> 1; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
+    }
+    if (g < groups && sub == 0) {
         const double cnt = (double)hw * cpg;
         const double m1 = a / cnt;
         double var = b / cnt - m1 * m1;
@@ -119,10 +132,39 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict_
     }
     __syncthreads();
     for (int c = threadIdx.x; c < cin; c += blockDim.x) {
-        const int g = c / cpg;
-        const float sc = gamma[c] * g_rstd[g];
+        const int gg = c / cpg;
+        const float sc = gamma[c] * g_rstd[gg];
         scale[(size_t)n * cin + c] = sc;
-        shift[(size_t)n * cin + c] = beta[c] - g_mean[g] * sc;
+        shift[(size_t)n * cin + c] = beta[c] - g_mean[gg] * sc;
+    }
+}
+
+// GroupNorm apply (+ SiLU): out[m][c] = act(x[m][c] * scale[n][c] + shift[n][c]),
+// reading a one- or two-source channel concat and writing the concatenation.
+// One 16-B chunk per thread, grid-stride; HBM-bound (2 B read + 2 B written / element).
+__global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
+                                                       int c1, int hw, size_t nchunks, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int silu, f16* __restrict__ out) {
+    const int cin = c0 + c1, nch = cin >> 3;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t pix = i / nch;
+        const int c = (int)(i - pix * nch) * 8;
+        const int n = (int)(pix / hw);
+        const f16* src = (c < c0) ? (s0 + pix * c0 + c) : (s1 + pix * c1 + (c - c0));
+        const f16x8 v = *reinterpret_cast<const f16x8*>(src);
+        const float4* sc = reinterpret_cast<const float4*>(scale + (size_t)n * cin + c);
+        const float4* sh = reinterpret_cast<const float4*>(shift + (size_t)n * cin + c);
+        const float4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        f16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float y = fmaf((float)v[j], av[j], bv[j]);
+            if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+            o[j] = (f16)y;
+        }
+        *reinterpret_cast<f16x8*>(out + pix * cin + c) = o;
     }
 }
 
@@ -201,7 +243,13 @@ static int ln_dispatch(const void* x, int m, int c, int ld, float eps, float* st
 
 using namespace c2d;
 
-extern "C" size_t c2d_groupnorm_workspace_size(int n, int c) { return (size_t)n * c * 2 * sizeof(float); }
+static const int GN_ROWS_PER_BLOCK = 128;
+
+static int gn_blocks(int hw) { return (hw + GN_ROWS_PER_BLOCK - 1) / GN_ROWS_PER_BLOCK; }
+
+extern "C" size_t c2d_groupnorm_workspace_size(int n, int c, int hw) {
+    return (size_t)n * gn_blocks(hw) * c * 2 * sizeof(float);
+}
 
 extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups,
                                    float eps, const float* gamma, const float* beta, float* scale, float* shift,
@@ -210,15 +258,14 @@ extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, i
     if (c1 > 0 && !src1) return C2D_E_ARG;
     const int cin = c0 + c1;
     if ((c0 & 7) || (c1 & 7) || cin <= 0 || groups <= 0 || groups > 128 || cin % groups) return C2D_E_SHAPE;
-    if (cin > 4096 || n <= 0 || hw <= 0) return C2D_E_SHAPE;
+    if (cin > 4096 || n <= 0 || hw <= 0 || (256 % groups) || 256 / groups > 64) return C2D_E_SHAPE;
     if (!aligned16(src0) || (src1 && !aligned16(src1))) return C2D_E_ALIGN;
     hipStream_t s = (hipStream_t)stream;
-    hipMemsetAsync(ws, 0, c2d_groupnorm_workspace_size(n, cin), s);
     const int nch = cin >> 3;
     const int cpg = cin / groups;
-    // ~128 pixels per block, at least one block per image
-    const int rows_per_block = 128;
-    dim3 grid((hw + rows_per_block - 1) / rows_per_block, n);
+    const int rows_per_block = GN_ROWS_PER_BLOCK;
+    const int nblk = gn_blocks(hw);
+    dim3 grid(nblk, n);
     if (nch <= 256) {
         const int R = 256 / nch;
         const size_t lds = (size_t)R * cin * 2 * sizeof(float);
@@ -229,7 +276,7 @@ extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, i
                            hw, cpg, rows_per_block, (float*)ws);
     }
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(n), dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1, hw,
-                       groups, eps, gamma, beta, (const float*)ws, scale, shift);
+                       groups, nblk, eps, gamma, beta, (const float*)ws, scale, shift);
     return check_launch();
 }
 
@@ -248,4 +295,19 @@ extern "C" int c2d_layernorm(const void* x, int m, int c, int ld, float eps, con
     if (!aligned16(x) || !aligned16(out)) return C2D_E_ALIGN;
     if (m <= 0) return C2D_OK;
     return ln_dispatch<true>(x, m, c, ld, eps, nullptr, gamma, beta, out, out_ld, (hipStream_t)stream);
+}
+
+extern "C" int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, int c1, int n, int hw,
+                                   const float* scale, const float* shift, int silu, void* out, void* stream) {
+    if (!src0 || !scale || !shift || !out) return C2D_E_ARG;
+    if (c1 > 0 && !src1) return C2D_E_ARG;
+    if ((c0 & 7) || (c1 & 7) || c0 + c1 <= 0 || n <= 0 || hw <= 0) return C2D_E_SHAPE;
+    if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out) || !aligned16(scale) || !aligned16(shift))
+        return C2D_E_ALIGN;
+    const size_t nchunks = (size_t)n * hw * ((c0 + c1) >> 3);
+    const size_t want = (nchunks + 255) / 256;
+    const unsigned blocks = (unsigned)(want < 8192 ? want : 8192);
+    hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
+                       (const f16*)src1, c0, c1, hw, nchunks, scale, shift, silu, (f16*)out);
+    return check_launch();
 }

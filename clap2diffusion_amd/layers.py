@@ -80,6 +80,10 @@ class HGroupNorm(nn.Module):
     def stats(self, x: torch.Tensor, x2: torch.Tensor | None = None):
         return ops.group_norm_stats(x, self.num_groups, self.eps, self.weight, self.bias, x2=x2)
 
+    def apply(self, x: torch.Tensor, x2: torch.Tensor | None = None, silu: bool = False) -> torch.Tensor:
+        """act(GroupNorm(cat[x, x2])) materialised once (stats + apply kernels)."""
+        return ops.group_norm_apply(x, self.stats(x, x2), silu, x2=x2)
+
 
 class HLayerNorm(nn.Module):
     def __init__(self, c: int, eps: float = 1e-5):

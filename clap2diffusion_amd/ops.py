@@ -128,11 +128,26 @@ def group_norm_stats(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tens
     c = c0 + c1
     scale = torch.empty((n, c), device=x.device, dtype=torch.float32)
     shift = torch.empty_like(scale)
-    ws = torch.empty((n, c, 2), device=x.device, dtype=torch.float32)
+    ws = torch.empty(lib().c2d_groupnorm_workspace_size(n, c, hw) // 4, device=x.device, dtype=torch.float32)
     rc = lib().c2d_groupnorm_stats(ptr(x), ptr(x2), c0, c1, n, hw, groups, eps, ptr(gamma), ptr(beta),
                                    ptr(scale), ptr(shift), ptr(ws), stream_ptr())
     check(rc, "c2d_groupnorm_stats")
     return scale, shift
+
+
+def group_norm_apply(x: torch.Tensor, gn, silu: bool, x2: torch.Tensor | None = None,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
+    """Materialise act(GroupNorm(cat[x, x2])) from the folded (scale, shift) tables."""
+    _require(x, "x")
+    n, c0 = x.shape[0], x.shape[-1]
+    c1 = x2.shape[-1] if x2 is not None else 0
+    hw = x.numel() // (n * c0)
+    if out is None:
+        out = torch.empty((*x.shape[:-1], c0 + c1), device=x.device, dtype=F16)
+    rc = lib().c2d_groupnorm_apply(ptr(x), ptr(x2), c0, c1, n, hw, ptr(gn[0]), ptr(gn[1]), int(silu), ptr(out),
+                                   stream_ptr())
+    check(rc, "c2d_groupnorm_apply")
+    return out
 
 
 def layer_norm_stats(x2d: torch.Tensor, eps: float) -> torch.Tensor:

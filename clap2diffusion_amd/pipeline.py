@@ -1,0 +1,243 @@
+"""AudioToImageInference — drop-in for the reference scripts/inference.py API.
+
+Same class, constructor, methods and CLI flags as the reference
+(scripts/inference.py:21-216): load_models, load_audio, extract_clap_embedding,
+apply_normalization, generate, batch_generate, main(--audio --text --output
+--checkpoint_dir --steps --cfg_scale --seed --no_hierarchical).  Where the
+reference stubs the CLAP embedding (:85-90) and the image (:161-164), this
+runs the real path:
+  audio -> ClapFeatureExtractor (CPU) -> HTSAT (HIP) -> ImprovedHierarchicalAudioEncoder
+  -> routed {early, mid, late} tokens -> 16 AudioAttnProcessor cross-attentions
+  -> 50-step CFG+DDIM on the HIP UNet (captured hipGraph) -> VAE decode -> PIL image.
+Composition contract: ehs = CLIP([uncond "", prompt]);
+routed tokens repeated for both CFG halves; adapter + Norm-60 and the legacy
+HierarchicalAudioV4 outputs are computed for API fidelity but not fed to the UNet.
+Checkpoints are loaded when present (audio_projector_stage2.pth 'adapter_state_dict',
+hierarchical_v4_final.pth), otherwise every network uses seeded synthetic weights.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import wave
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from . import weights as W
+from .htsat import HTSATEncoder
+from .processor import AudioProcessorManager
+from .projectors import AudioAdapter, HierarchicalAudioV4, ImprovedHierarchicalAudioEncoder, normalize_tokens
+from .sampler import GraphDenoiser
+from .scheduler import DDIMScheduler
+from .text_encoder import TextEncoder, tokenize
+from .unet import UNet2DConditionModel
+from .vae import VAEDecoder
+
+SR = 48000
+
+
+def synthetic_thunder(seed: int = 0, seconds: float = 10.0, sr: int = SR) -> np.ndarray:
+    """SURVEY.md §8(d) stand-in for the LFS-stub assets/Thunder.wav: low-passed white
+    noise with three exponentially decaying bursts, peak-normalised."""
+    from scipy.signal import lfilter
+    rs = np.random.RandomState(seed)
+    n = int(seconds * sr)
+    y = lfilter([0.005], [1.0, -0.995], rs.randn(n))  # 1-pole IIR low-pass, a = 0.995
+    t = np.arange(n) / sr
+    env = 0.05 + sum(np.where(t >= t0, np.exp(-(t - t0) / 0.6), 0.0) for t0 in (1.0, 4.5, 7.0))
+    y = y * env
+    return (y / (np.abs(y).max() + 1e-8)).astype(np.float32)
+
+
+def _read_wav(path: str) -> tuple[np.ndarray, int]:
+    with wave.open(str(path), "rb") as f:
+        sr, ch, sw, n = f.getframerate(), f.getnchannels(), f.getsampwidth(), f.getnframes()
+        raw = f.readframes(n)
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32}[sw]
+    x = np.frombuffer(raw, dtype=dt).astype(np.float32)
+    if sw == 1:
+        x = (x - 128.0) / 128.0
+    else:
+        x /= float(2 ** (8 * sw - 1))
+    return x.reshape(-1, ch).mean(axis=1), sr
+
+
+class AudioToImageInference:
+    def __init__(self, checkpoint_dir="../checkpoints", device=None, seed: int = 0, height: int = 512,
+                 width: int = 512, use_graph: bool = True, verbose: bool = True):
+        self.checkpoint_dir = Path(checkpoint_dir)
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("the sampling path runs on the HIP kernels only (MI355X); no CPU fallback")
+        self.seed, self.height, self.width = seed, height, width
+        self.use_graph, self.verbose = use_graph, verbose
+        self.load_models()
+        self.OPTIMAL_NORM = 60.0
+        self._denoisers = {}
+
+    # ------------------------------------------------------------ models
+    def _log(self, *a):
+        if self.verbose:
+            print(*a)
+
+    def load_models(self):
+        dev = self.device
+        self._log(f"Initializing inference pipeline on {dev}")
+        self.unet = UNet2DConditionModel().to(dev)
+        self.unet.load_diffusers_state_dict(W.synth_unet(self.seed))
+        self.manager = AudioProcessorManager(self.unet)
+        self.manager.setup_processors(verbose=self.verbose)
+        for level, p in self.manager.level_processors().items():
+            p.load_state_dict(W.synth_processor_weights(level, self.seed))
+            p.to(dev).eval()
+        self.clap = HTSATEncoder().to(dev)
+        self.clap.load_clap_state_dict(W.synth_htsat(self.seed))
+        self.hier_encoder = W.fill_module(ImprovedHierarchicalAudioEncoder(), "improved.", self.seed).to(dev).eval()
+        adapter_path = self.checkpoint_dir / "audio_projector_stage2.pth"
+        self.audio_adapter = W.fill_module(AudioAdapter(), "adapter.", self.seed).to(dev).eval()
+        if adapter_path.exists():
+            self._log(f"Loading Audio Adapter from {adapter_path}")
+            ck = torch.load(adapter_path, map_location=dev, weights_only=True)
+            if "adapter_state_dict" in ck:
+                self.audio_adapter.load_state_dict(ck["adapter_state_dict"])
+        self.hierarchical_model = W.fill_module(HierarchicalAudioV4(), "v4.", self.seed).to(dev).eval()
+        hpath = self.checkpoint_dir / "hierarchical_v4_final.pth"
+        if hpath.exists():
+            self._log(f"Loading Hierarchical Model from {hpath}")
+            self.hierarchical_model.load_state_dict(torch.load(hpath, map_location=dev, weights_only=True))
+        self.text_encoder = TextEncoder(dev, seed=self.seed)
+        self.vae = VAEDecoder().to(dev)
+        self.vae.load_diffusers_state_dict(W.synth_vae_decoder(self.seed))
+        self.scheduler = DDIMScheduler()
+        from transformers import ClapFeatureExtractor
+        self.feature_extractor = ClapFeatureExtractor(truncation="rand_trunc", padding="repeatpad")
+
+    # ------------------------------------------------------------ reference API
+    def load_audio(self, audio_path, duration=10):
+        if str(audio_path).startswith("synthetic:"):
+            audio = synthetic_thunder(int(str(audio_path).split(":", 1)[1] or 0), duration)
+        else:
+            x, sr = _read_wav(audio_path)
+            if sr != SR:
+                from scipy.signal import resample_poly
+                g = np.gcd(sr, SR)
+                x = resample_poly(x, SR // g, sr // g).astype(np.float32)
+            audio = x[: int(duration * SR)]
+        return audio / (np.abs(audio).max() + 1e-8)
+
+    def mel_features(self, audios: list) -> torch.Tensor:
+        f = self.feature_extractor(audios, sampling_rate=SR, return_tensors="np")["input_features"]
+        return torch.from_numpy(f[:, 0]).to(self.device)  # [B, 1001, 64]
+
+    def extract_clap_embedding(self, audio) -> torch.Tensor:
+        audios = audio if isinstance(audio, list) else [audio]
+        return self.clap(self.mel_features(audios))
+
+    def apply_normalization(self, audio_tokens, target_norm=60.0):
+        return normalize_tokens(audio_tokens, target_norm)
+
+    @torch.no_grad()
+    def generate(self, audio_path, text_prompt="", num_inference_steps=50, guidance_scale=7.5, seed=None,
+                 use_hierarchical=True):
+        if seed is not None:
+            torch.manual_seed(seed)
+            np.random.seed(seed)
+        audio = self.load_audio(audio_path)
+        img = self.generate_batch(self.mel_features([audio]), [text_prompt], num_inference_steps, guidance_scale,
+                                  seeds=[0 if seed is None else seed], use_hierarchical=use_hierarchical)
+        return self.to_pil(img)[0]
+
+    def batch_generate(self, audio_paths, text_prompts=None, **kwargs):
+        if text_prompts is None:
+            text_prompts = [""] * len(audio_paths)
+        steps = kwargs.get("num_inference_steps", 50)
+        g = kwargs.get("guidance_scale", 7.5)
+        seed = kwargs.get("seed", None)
+        mel = self.mel_features([self.load_audio(p) for p in audio_paths])
+        seeds = [(0 if seed is None else seed) * 1000 + i for i in range(len(audio_paths))]
+        img = self.generate_batch(mel, list(text_prompts), steps, g, seeds=seeds,
+                                  use_hierarchical=kwargs.get("use_hierarchical", True))
+        return self.to_pil(img)
+
+    # ------------------------------------------------------------ batched core
+    def initial_latents(self, seeds: list[int]) -> torch.Tensor:
+        """Per-sample CPU generator (seed) -> identical latents on any number of GPUs."""
+        h, w = self.height // 8, self.width // 8
+        lat = [torch.randn(4, h, w, generator=torch.Generator().manual_seed(int(s))) for s in seeds]
+        return torch.stack(lat).to(self.device)
+
+    def denoiser(self, b: int, steps: int, guidance: float, ehs, audio_kwargs) -> GraphDenoiser:
+        key = (b, steps, float(guidance))
+        d = self._denoisers.get(key)
+        if d is None:
+            sch = DDIMScheduler()
+            sch.set_timesteps(steps)
+            d = GraphDenoiser(self.unet, sch, b, self.height // 8, self.width // 8, guidance, ehs, audio_kwargs,
+                              use_graph=self.use_graph)
+            self._denoisers[key] = d
+        return d
+
+    @torch.no_grad()
+    def condition(self, mel: torch.Tensor, ids_uncond: torch.Tensor, ids_cond: torch.Tensor,
+                  use_hierarchical: bool = True):
+        """mel [B,T,64] -> (ehs [2B,77,768], routed audio kwargs, extras)."""
+        clap = self.clap(mel)
+        b = clap.shape[0]
+        extras = {}
+        adapter_tokens = self.apply_normalization(self.audio_adapter(clap), self.OPTIMAL_NORM)
+        extras["adapter_tokens"] = adapter_tokens
+        if use_hierarchical:
+            extras["tokens_77"], extras["hierarchy"] = self.hierarchical_model(clap, return_intermediate=True)
+        _, info = self.hier_encoder(clap, return_all=True)
+        routed = {k: torch.cat([v, v], 0).to(torch.float16).contiguous() for k, v in info["routed"].items()}
+        ehs = self.text_encoder(torch.cat([ids_uncond, ids_cond], 0))
+        extras["clap"] = clap
+        return ehs, self.manager.get_audio_kwargs(routed), extras
+
+    @torch.no_grad()
+    def generate_batch(self, mel: torch.Tensor, prompts: list[str] | None, num_inference_steps: int = 50,
+                       guidance_scale: float = 7.5, seeds: list[int] | None = None, use_hierarchical: bool = True,
+                       ids: tuple | None = None, latents: torch.Tensor | None = None) -> torch.Tensor:
+        """mel [B, 1001, 64] on device -> uint8 images NHWC [B, H, W, 3] on device."""
+        b = mel.shape[0]
+        if ids is None:
+            ids = (tokenize([""] * b, self.device), tokenize(prompts or [""] * b, self.device))
+        ehs, kw, _ = self.condition(mel, ids[0], ids[1], use_hierarchical)
+        if latents is None:
+            latents = self.initial_latents(seeds if seeds is not None else list(range(b)))
+        den = self.denoiser(b, num_inference_steps, guidance_scale, ehs, kw)
+        den.ehs.copy_(ehs)
+        for k, v in kw["audio"].items():
+            den.kw["audio"][k].copy_(v)
+        x = den.run(latents * self.scheduler.init_noise_sigma)
+        return self.vae(x)
+
+    @staticmethod
+    def to_pil(images: torch.Tensor):
+        from PIL import Image
+        return [Image.fromarray(im) for im in images.cpu().numpy()]
+
+
+def main():
+    ap = argparse.ArgumentParser(description="CLAP2Diffusion Inference (MI355X HIP path)")
+    ap.add_argument("--audio", type=str, required=True, help="Path to audio file (or synthetic:<seed>)")
+    ap.add_argument("--text", type=str, default="", help="Text prompt")
+    ap.add_argument("--output", type=str, default="output.png", help="Output image path")
+    ap.add_argument("--checkpoint_dir", type=str, default="../checkpoints", help="Checkpoint directory")
+    ap.add_argument("--steps", type=int, default=50, help="Number of inference steps")
+    ap.add_argument("--cfg_scale", type=float, default=7.5, help="Guidance scale")
+    ap.add_argument("--seed", type=int, default=None, help="Random seed")
+    ap.add_argument("--no_hierarchical", action="store_true", help="Disable hierarchical processing")
+    a = ap.parse_args()
+    pipe = AudioToImageInference(checkpoint_dir=a.checkpoint_dir)
+    img = pipe.generate(audio_path=a.audio, text_prompt=a.text, num_inference_steps=a.steps,
+                        guidance_scale=a.cfg_scale, seed=a.seed, use_hierarchical=not a.no_hierarchical)
+    img.save(a.output)
+    print(f"Image saved to {a.output}")
+
+
+if __name__ == "__main__":
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    main()

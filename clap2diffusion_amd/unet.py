@@ -9,14 +9,18 @@ The module tree and attribute names follow diffusers 0.23.1 so that
 
 Per-step structure: conv_in, 4 down blocks, mid block, 4 up
 blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
-  ResnetBlock2D   GN1 stats -> conv1 (GN1+SiLU prologue, bias+temb epilogue) ->
-                  GN2 stats -> conv2 (GN2+SiLU prologue, bias+residual epilogue);
-                  skip concat read from two sources (never materialised);
+  ResnetBlock2D   GN1 stats + apply(SiLU) over the (two-source) skip concat ->
+                  conv1 (bias + temb epilogue) -> GN2 stats + apply(SiLU) ->
+                  conv2 (bias + residual epilogue); the 1x1 shortcut reads the raw
+                  skip concat from its two sources (never materialised);
                   all 22 time_emb_proj GEMMs batched into one (SiLU prologue).
-  Transformer2D   GN stats -> proj_in (GN prologue) -> block -> proj_out (+residual).
+  Transformer2D   GN stats + apply -> proj_in -> block -> proj_out (+residual).
   Block           LN1 -> fused QKV GEMM -> flash attn -> to_out (+residual);
                   LN2 -> audio cross-attn processor (+residual);
-                  FF: GEGLU GEMM with the LN3 prologue -> Linear (+residual).
+                  LN3 -> GEGLU GEMM (h*gelu(g) epilogue) -> Linear (+residual).
+  Normalised activations are materialised once per norm (HBM-bound kernels):
+  re-normalising inside the consumer GEMM would redo the affine+SiLU in all 9
+  taps of a 3x3 conv / every N-tile of a GEMM, which is VALU-bound on CDNA4.
   Up/Downsample   nearest-x2 gather and stride-2 folded into the conv addressing.
 """
 from __future__ import annotations
@@ -136,7 +140,7 @@ class BasicTransformerBlock(nn.Module):
         h = self._attend(self.attn2, self.norm2(h), h, ehs, kw)
         b, l, c = h.shape
         h2 = h.view(b * l, c)
-        ff1 = self.ff.net[0].proj(h2, ln=self.norm3.prologue(h2), act="geglu")
+        ff1 = self.ff.net[0].proj(self.norm3(h2), act="geglu")
         self.ff.net[2](ff1, resid=h2, out=h2)
         return h
 
@@ -151,7 +155,7 @@ class Transformer2DModel(nn.Module):
 
     def forward(self, x, ehs, cross_attention_kwargs):
         n, hh, ww, c = x.shape
-        h = self.proj_in(x, gn=self.norm.stats(x), gn_silu=False)
+        h = self.proj_in(self.norm.apply(x))
         t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs)
         return self.proj_out(t.view(n, hh, ww, c), resid=x)
 
@@ -170,14 +174,12 @@ class ResnetBlock2D(nn.Module):
         self.temb_off = None  # column offset into the batched time_emb_proj output
 
     def forward(self, x, temb_all=None, skip=None):
-        sc1 = self.norm1.stats(x, skip)
         temb = None
         if temb_all is not None:
             temb = temb_all[:, self.temb_off:self.temb_off + self.cout]
-        h = self.conv1(x, x2=skip, gn=sc1, gn_silu=True, temb=temb)
-        sc2 = self.norm2.stats(h)
+        h = self.conv1(self.norm1.apply(x, skip, silu=True), temb=temb)
         res = self.conv_shortcut(x, x2=skip) if self.conv_shortcut is not None else x
-        return self.conv2(h, gn=sc2, gn_silu=True, resid=res)
+        return self.conv2(self.norm2.apply(h, silu=True), resid=res)
 
 
 class Downsample2D(nn.Module):
@@ -353,7 +355,7 @@ class UNet2DConditionModel(nn.Module):
                     h = blk.attentions[j](h, ehs, kw)
             if hasattr(blk, "upsamplers"):
                 h = blk.upsamplers[0](h)
-        return self.conv_out(h, gn=self.conv_norm_out.stats(h), gn_silu=True)
+        return self.conv_out(self.conv_norm_out.apply(h, silu=True))
 
     def forward(self, sample: torch.Tensor, timestep, encoder_hidden_states: torch.Tensor,
                 cross_attention_kwargs: dict | None = None, return_dict: bool = True):

@@ -298,3 +298,11 @@ def synth_generic(shapes, seed: int = 0, tag: str = "", device="cpu") -> "Ordere
 
 def synth_htsat(seed: int = 0, device="cpu") -> "OrderedDict[str, torch.Tensor]":
     return synth_generic(htsat_param_shapes(), seed, "htsat.", device)
+
+
+def fill_module(module, tag: str, seed: int = 0, keep=("decomposer.temperature", "decomposer.level_prior")):
+    """Deterministically (re)initialise every floating tensor of a torch module by key."""
+    sd = module.state_dict()
+    shapes = {k: tuple(v.shape) for k, v in sd.items() if v.is_floating_point() and k not in keep}
+    module.load_state_dict({**sd, **synth_generic(shapes, seed, tag)})
+    return module

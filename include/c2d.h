@@ -99,14 +99,24 @@ int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
  *   scale[n][c] = gamma[c]*rstd[n,g(c)], shift[n][c] = beta[c] - mean[n,g(c)]*scale[n][c]
  * Input may be a two-source channel concat (GroupNorm over the concatenation,
  * groups may straddle the seam).  ws: fp32 workspace of
- * c2d_groupnorm_workspace_size(n, c) bytes; it is zeroed inside (memset node).
+ * c2d_groupnorm_workspace_size(n, c, hw) bytes holding per-block partial moments
+ * (plain stores, fixed-order reduction: deterministic, no atomics, no memset).
  * Replaces torch.nn.GroupNorm in ResnetBlock2D.norm1/norm2 (eps 1e-5) and
  * Transformer2DModel.norm (eps 1e-6), diffusers 0.23.1.
  */
-size_t c2d_groupnorm_workspace_size(int n, int c);
+size_t c2d_groupnorm_workspace_size(int n, int c, int hw);
 int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, int c1, int n, int hw,
                         int groups, float eps, const float* gamma, const float* beta,
                         float* scale, float* shift, void* ws, void* stream);
+
+/*
+ * GroupNorm apply with the folded tables: out[m][c] = act(x[m][c]*scale[n][c] + shift[n][c]),
+ * act = SiLU when silu != 0; the input may be a two-source concat, the output is the
+ * concatenation (fp16 [n*hw][c0+c1]).  The UNet materialises each normalised tensor once
+ * (HBM-bound) instead of re-normalising it in every 3x3 tap / N-tile of the consuming GEMM.
+ */
+int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, int c1, int n, int hw,
+                        const float* scale, const float* shift, int silu, void* out, void* stream);
 
 /*
  * LayerNorm over rows of a row-major fp16 [m][c] matrix (leading dim ld).

@@ -258,3 +258,25 @@ def test_timestep_embedding(dev):
         a = t * freqs
         ref = torch.cat([torch.cos(a), torch.sin(a)]).expand(2, -1)
         close(out, ref, tol_max=2e-3, tol_l2=2e-3)
+
+
+@pytest.mark.parametrize("silu", [True, False])
+def test_groupnorm_apply_dual_source(dev, silu):
+    n, h, c0, c1 = 2, 16, 640, 320
+    x0, x1 = gen(n, c0, h, h, seed=50) + 1.0, gen(n, c1, h, h, seed=51) * 2
+    xc = torch.cat([x0, x1], 1)
+    gamma, beta = gen(c0 + c1, seed=52) * 0.1 + 1, gen(c0 + c1, seed=53) * 0.1
+    ref = F.group_norm(xc, 32, gamma, beta, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    a, b = nhwc(x0).half().to(dev), nhwc(x1).half().to(dev)
+    gn = ops.group_norm_stats(a, 32, 1e-5, gamma.float().to(dev), beta.float().to(dev), x2=b)
+    out = ops.group_norm_apply(a, gn, silu, x2=b)
+    close(nchw(out), ref)
+
+
+def test_groupnorm_deterministic(dev):
+    x = nhwc(gen(4, 320, 32, 32, seed=54)).half().to(dev)
+    g, b = torch.ones(320, device=dev), torch.zeros(320, device=dev)
+    r = [ops.group_norm_stats(x, 32, 1e-5, g, b)[0] for _ in range(3)]
+    assert all(torch.equal(r[0], t) for t in r[1:])
