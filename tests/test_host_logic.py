@@ -1,0 +1,91 @@
+"""CPU tests of the host-side logic: DDIM tables, weight layouts and packing,
+processor routing, HTSAT window maps, tokenisation, data-parallel sharding."""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from clap2diffusion_amd import ops
+from clap2diffusion_amd.htsat import _row_map, _shift_mask
+from clap2diffusion_amd.processor import AudioAttnProcessor, AudioProcessorManager
+from clap2diffusion_amd.scheduler import DDIMScheduler
+from clap2diffusion_amd.text_encoder import prompt_to_ids
+from clap2diffusion_amd.unet import UNet2DConditionModel
+from clap2diffusion_amd.weights import param_count, unet_param_shapes, vae_decoder_param_shapes
+from oracle import ddim_ref
+from oracle.htsat_ref import shift_mask
+
+
+def test_ddim_timesteps_and_coefficients():
+    s = DDIMScheduler()
+    s.set_timesteps(50)
+    ts = s.timesteps.tolist()
+    assert ts[0] == 981 and ts[-1] == 1 and len(ts) == 50 and all(a - b == 20 for a, b in zip(ts, ts[1:]))
+    s10 = DDIMScheduler()
+    s10.set_timesteps(10)
+    assert s10.timesteps.tolist() == [901, 801, 701, 601, 501, 401, 301, 201, 101, 1]
+    t_table, coef = s.device_tables("cpu")
+    ac = ddim_ref.alphas_cumprod()
+    assert torch.allclose(coef[0], torch.stack([ac[981], ac[961]]))
+    assert torch.allclose(coef[-1], torch.stack([ac[1], ac[0]]))   # set_alpha_to_one=False
+    x, e = torch.randn(1, 4, 8, 8), torch.randn(1, 4, 8, 8)
+    assert torch.allclose(s.step(e, 501, x).prev_sample, ddim_ref.ddim_step(e, 501, x, 50, ac))
+
+
+def test_unet_topology_matches_sd15():
+    shapes = unet_param_shapes()
+    assert len(shapes) == 686 and abs(param_count(shapes) / 1e6 - 859.52) < 0.01
+    assert abs(param_count(vae_decoder_param_shapes()) / 1e6 - 49.49) < 0.01
+
+
+def test_processor_level_routing_and_setup():
+    unet = UNet2DConditionModel()
+    mgr = AudioProcessorManager(unet)
+    assert len(unet.attn_processors) == 32
+    assert [len(mgr.level_mapping[k]) for k in ("early", "mid", "late")] == [4, 7, 5]
+    mgr.setup_processors(verbose=False)
+    procs = unet.attn_processors
+    shared = {id(p) for n, p in procs.items() if "attn2" in n}
+    assert len(shared) == 3                                      # one processor per level
+    assert all(isinstance(p, AudioAttnProcessor) for n, p in procs.items() if "attn2" in n)
+    assert not any(isinstance(p, AudioAttnProcessor) for n, p in procs.items() if "attn1" in n)
+    p = mgr.level_processors()["early"]
+    assert set(p.state_dict()) == {"alpha", "audio_proj.0.weight", "audio_proj.0.bias", "audio_proj.3.weight",
+                                   "audio_proj.3.bias"}
+    assert mgr.get_audio_kwargs({"early": 1}) == {"audio": {"early": 1}}
+
+
+def test_conv_weight_packing_matches_im2col():
+    w = torch.randn(16, 24, 3, 3)
+    x = torch.randn(1, 24, 5, 5)
+    wp, kp = ops.pack_conv_weight(w)
+    assert kp == 256 and wp.shape == (16, 256)
+    cols = F.unfold(F.pad(x, (1, 1, 1, 1)), 3)                   # [1, cin*9 (c-major), L]
+    cols = cols.view(24, 9, -1).permute(1, 0, 2).reshape(216, -1)  # -> (tap, cin) order
+    y = (wp[:, :216].float() @ cols).view(1, 16, 5, 5)
+    assert torch.allclose(y, F.conv2d(x, w, padding=1), atol=2e-2, rtol=2e-2)
+
+
+def test_geglu_interleave_roundtrip():
+    w, b = torch.randn(2 * 64, 8), torch.randn(2 * 64)
+    wi, bi = ops.geglu_interleave(w, b)
+    x = torch.randn(3, 8)
+    h, g = F.linear(x, w, b).chunk(2, -1)
+    yi = F.linear(x, wi, bi).view(3, 64 // 16, 2, 16)
+    assert torch.allclose(yi[:, :, 0].reshape(3, 64), h) and torch.allclose(yi[:, :, 1].reshape(3, 64), g)
+
+
+def test_htsat_window_maps_match_roll_partition():
+    b, h, win, shift = 2, 16, 8, 4
+    rows = _row_map(b, h, h, win, shift)
+    x = torch.arange(b * h * h).view(b, h, h, 1)
+    y = torch.roll(x, (-shift, -shift), (1, 2)).view(b, h // win, win, h // win, win, 1)
+    y = y.permute(0, 1, 3, 2, 4, 5).reshape(-1)
+    assert np.array_equal(rows, y.numpy())
+    assert np.array_equal(_shift_mask(h, h, win, shift), shift_mask(h, h, win, shift).numpy())
+
+
+def test_prompt_ids_deterministic():
+    ids = prompt_to_ids("a beach")
+    assert len(ids) == 77 and ids[0] == 49406 and ids[3] == 49407 and ids == prompt_to_ids("A beach")
