@@ -15,6 +15,7 @@
 // A and B tiles are register-staged (load early, transform, ds_write_b128 late)
 // into a double-buffered, XOR-swizzled LDS image: one barrier per K step.
 #include "common.h"
+#include <stdlib.h>
 
 namespace c2d {
 
@@ -107,6 +108,82 @@ __device__ __forceinline__ f16x8 apply_pro(const IgemmParams& p, f16x8 v, int n,
         for (int i = 0; i < 8; ++i) v[i] = (f16)silu_f((float)v[i]);
     }
     return v;
+}
+
+// ---- epilogue: lane holds out[row = m-tile row (lane&15)][cols 4*(lane>>4) .. +3]
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue(const IgemmParams& p, f32x4 (&acc)[BN / 32][BM / 32], int m0, int n0, int wm,
+                                         int wn, int lane) {
+    constexpr int TM = BM / 32, TN = BN / 32;
+    const int hw = p.oh * p.ow;
+    const bool geglu = (p.act == C2D_ACT_GEGLU);
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+        const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
+        if (m >= p.M) continue;
+        const int nimg = m / hw;
+        if (!geglu) {
+#pragma unroll
+            for (int a = 0; a < TN; ++a) {
+                const int j = n0 + wn * (BN / 2) + a * 16 + 4 * (lane >> 4);
+                if (j >= p.cout) continue;
+                float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+                if (p.bias) {
+                    float4 bb = *reinterpret_cast<const float4*>(p.bias + j);
+                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
+                    else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+                    else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
+                }
+                if (p.temb) {
+                    f16x4 t = *reinterpret_cast<const f16x4*>(p.temb + (size_t)nimg * p.temb_ld + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                if (p.resid) {
+                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                f16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+            }
+        } else {
+            // packed rows: [16 h | 16 g] per 32-row block -> 16 output features
+#pragma unroll
+            for (int a = 0; a < TN; a += 2) {
+                const int jp = n0 + wn * (BN / 2) + a * 16;  // packed row of the h block
+                if (jp >= p.cout) continue;
+                const int jo = (jp >> 1) + 4 * (lane >> 4);  // output feature
+                const int jh = jp + 4 * (lane >> 4), jg = jh + 16;
+                float hv[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+                float gv[4] = {acc[a + 1][b][0], acc[a + 1][b][1], acc[a + 1][b][2], acc[a + 1][b][3]};
+                if (p.bias) {
+                    float4 bh = *reinterpret_cast<const float4*>(p.bias + jh);
+                    float4 bg = *reinterpret_cast<const float4*>(p.bias + jg);
+                    hv[0] += bh.x; hv[1] += bh.y; hv[2] += bh.z; hv[3] += bh.w;
+                    gv[0] += bg.x; gv[1] += bg.y; gv[2] += bg.z; gv[3] += bg.w;
+                }
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = hv[r] * gelu_f(gv[r]);
+                if (p.resid) {
+                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + jo);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                f16x4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + jo) = o;
+            }
+        }
+    }
 }
 
 template <int BM, int BN, int AMODE>
@@ -222,75 +299,132 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgemmParams p) {
         __syncthreads();
     }
 
-    // ---- epilogue: lane holds out[row = m-tile row (lane&15)][cols 4*(lane>>4) .. +3]
-    const bool geglu = (p.act == C2D_ACT_GEGLU);
+    epilogue<BM, BN>(p, acc, m0, n0, wm, wn, lane);
+}
+
+
+// ---------------------------------------------------------------------------
+// LDS-DMA pipeline (no prologue): A and B tiles go HBM -> LDS with
+// global_load_lds_dwordx4 (16 B per lane, one 1-KiB wave instruction per 8 rows),
+// double-buffered, so the next K step streams in while this one runs on MFMA,
+// with no staging VGPRs and no ds_write.  The LDS image is lane-linear, so the
+// XOR bank swizzle is applied to the per-lane SOURCE chunk (lane slot s of row r
+// fetches logical chunk s ^ f(r)) and undone on the read (lds_off).  Padding /
+// out-of-range lanes fetch from a zero page, so halo and tails need no masking.
+__device__ __attribute__((aligned(64))) f16 c2d_zero_page[64];
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+template <int BM, int BN, int AMODE>
+__global__ void __launch_bounds__(256) igemm_glds_kernel(IgemmParams p) {
+    constexpr int TM = BM / 32, TN = BN / 32;
+    constexpr int AI = BM / 32, BI = BN / 32;        // glds instructions per wave per K step
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int tile = xcd_remap(blockIdx.x, p.gx * p.gy);
+    const int mt = tile / p.gx, nt = tile - mt * p.gx;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int lrow = lane >> 3, slot = lane & 7;
+    const f16* zero = c2d_zero_page;
+    const int hw = p.oh * p.ow;
+
+    int a_n[AI], a_iy[AI], a_ix[AI], a_c[AI];
+    bool a_ok[AI];
 #pragma unroll
-    for (int b = 0; b < TM; ++b) {
-        const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
-        if (m >= p.M) continue;
-        const int nimg = m / hw;
-        if (!geglu) {
+    for (int i = 0; i < AI; ++i) {
+        const int row = (wave * AI + i) * 8 + lrow;
+        const int m = m0 + row;
+        a_ok[i] = m < p.M;
+        const int mm = a_ok[i] ? m : 0;
+        const int nn = mm / hw, r = mm - nn * hw;
+        const int oy = r / p.ow, ox = r - oy * p.ow;
+        a_n[i] = nn;
+        a_iy[i] = oy * p.stride - p.pad;
+        a_ix[i] = ox * p.stride - p.pad;
+        a_c[i] = slot ^ ((row >> 1) & 7);
+    }
+    const f16* b_src[BI];
 #pragma unroll
-            for (int a = 0; a < TN; ++a) {
-                const int j = n0 + wn * (BN / 2) + a * 16 + 4 * (lane >> 4);
-                if (j >= p.cout) continue;
-                float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-                if (p.bias) {
-                    float4 bb = *reinterpret_cast<const float4*>(p.bias + j);
-                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-                }
+    for (int i = 0; i < BI; ++i) {
+        const int row = (wave * BI + i) * 8 + lrow;
+        const int j = n0 + row;
+        b_src[i] = (j < p.cout) ? p.wt + (size_t)j * p.kpad + (slot ^ ((row >> 1) & 7)) * 8 : nullptr;
+    }
+
+    auto issue = [&](int kt, int buf) {
+        const int k0 = kt * 64;
+        int ky = 0, kx = 0, cbase = k0;
+        if (AMODE == AM_3X3_FAST) {
+            const int tap = k0 / p.cin;
+            cbase = k0 - tap * p.cin;
+            ky = tap / 3;
+            kx = tap - ky * 3;
+        }
+        char* base = smem + buf * STAGE;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
-                    else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
-                    else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
-                }
-                if (p.temb) {
-                    f16x4 t = *reinterpret_cast<const f16x4*>(p.temb + (size_t)nimg * p.temb_ld + j);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
-                }
-                if (p.resid) {
-                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
-                }
-                f16x4 o;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
-                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+        for (int i = 0; i < AI; ++i) {
+            const int c = cbase + a_c[i] * 8;
+            const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
+            const bool v = a_ok[i] && c < p.cin && iy >= 0 && iy < p.vh && ix >= 0 && ix < p.vw;
+            const f16* src = zero;
+            if (v) {
+                const int sy = p.up ? (iy >> 1) : iy, sx = p.up ? (ix >> 1) : ix;
+                const size_t pix = ((size_t)a_n[i] * p.h + sy) * p.w + sx;
+                src = (c < p.c0) ? (p.src0 + pix * p.c0 + c) : (p.src1 + pix * p.c1 + (c - p.c0));
             }
-        } else {
-            // packed rows: [16 h | 16 g] per 32-row block -> 16 output features
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + (wave * AI + i) * 1024), 16, 0, 0);
+        }
 #pragma unroll
-            for (int a = 0; a < TN; a += 2) {
-                const int jp = n0 + wn * (BN / 2) + a * 16;  // packed row of the h block
-                if (jp >= p.cout) continue;
-                const int jo = (jp >> 1) + 4 * (lane >> 4);  // output feature
-                const int jh = jp + 4 * (lane >> 4), jg = jh + 16;
-                float hv[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-                float gv[4] = {acc[a + 1][b][0], acc[a + 1][b][1], acc[a + 1][b][2], acc[a + 1][b][3]};
-                if (p.bias) {
-                    float4 bh = *reinterpret_cast<const float4*>(p.bias + jh);
-                    float4 bg = *reinterpret_cast<const float4*>(p.bias + jg);
-                    hv[0] += bh.x; hv[1] += bh.y; hv[2] += bh.z; hv[3] += bh.w;
-                    gv[0] += bg.x; gv[1] += bg.y; gv[2] += bg.z; gv[3] += bg.w;
-                }
-                float v[4];
+        for (int i = 0; i < BI; ++i) {
+            const f16* src = b_src[i] ? b_src[i] + k0 : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + A_BYTES + (wave * BI + i) * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[TN][TM];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = hv[r] * gelu_f(gv[r]);
-                if (p.resid) {
-                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + jo);
+    for (int a = 0; a < TN; ++a)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
-                }
-                f16x4 o;
+        for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = p.kpad / 64;
+    issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // stage kt landed for every wave; every wave is done reading stage kt-1
+        if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+        const char* As = smem + buf * STAGE;
+        const char* Bs = As + A_BYTES;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
-                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + jo) = o;
-            }
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + (lane >> 4);
+            f16x8 fa[TM], fb[TN];
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+                fa[t] = *reinterpret_cast<const f16x8*>(As + lds_off(wm * (BM / 2) + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int t = 0; t < TN; ++t)
+                fb[t] = *reinterpret_cast<const f16x8*>(Bs + lds_off(wn * (BN / 2) + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
         }
     }
+    epilogue<BM, BN>(p, acc, m0, n0, wm, wn, lane);
+}
+
+template <int BM, int BN, int AMODE>
+static void launch_glds(const IgemmParams& p, hipStream_t s) {
+    const int smem = 2 * (BM + BN) * 128;
+    hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, AMODE>), dim3(p.gx * p.gy), dim3(256), smem, s, p);
 }
 
 template <int BM, int BN, int AMODE>
@@ -303,6 +437,13 @@ static void launch(const IgemmParams& p, hipStream_t s) {
 }  // namespace c2d
 
 using namespace c2d;
+
+// C2D_NO_GLDS=1 forces the register-staged kernel (A/B comparisons, debugging)
+static bool getenv_noglds() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_NO_GLDS"); v = (e && e[0] == '1') ? 1 : 0; }
+    return v == 1;
+}
 
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     if (!d || !d->src0 || !d->weight || !d->out) return C2D_E_ARG;
@@ -351,17 +492,24 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
 
     hipStream_t s = (hipStream_t)stream;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
+    const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !getenv_noglds();
     // small problems: 64x64 tiles to fill 256 CUs
     const long tiles128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     const bool small = tiles128 < 512;
     if (small) {
         p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
-        if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);
+        if (dma) {
+            if (amode == AM_1X1) launch_glds<64, 64, AM_1X1>(p, s);
+            else launch_glds<64, 64, AM_3X3_FAST>(p, s);
+        } else if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);
         else if (amode == AM_3X3_FAST) launch<64, 64, AM_3X3_FAST>(p, s);
         else launch<64, 64, AM_3X3_GEN>(p, s);
     } else {
         p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
-        if (amode == AM_1X1) launch<128, 128, AM_1X1>(p, s);
+        if (dma) {
+            if (amode == AM_1X1) launch_glds<128, 128, AM_1X1>(p, s);
+            else launch_glds<128, 128, AM_3X3_FAST>(p, s);
+        } else if (amode == AM_1X1) launch<128, 128, AM_1X1>(p, s);
         else if (amode == AM_3X3_FAST) launch<128, 128, AM_3X3_FAST>(p, s);
         else launch<128, 128, AM_3X3_GEN>(p, s);
     }

@@ -1,0 +1,49 @@
+"""Per-shape timing of c2d_conv2d_igemm on the UNet's hot conv/GEMM shapes (N = 16)."""
+import math
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from clap2diffusion_amd import ops  # noqa: E402
+
+dev = torch.device("cuda")
+N = 16
+SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)
+    ("L0 conv3x3 320", 3, 64, 320, 320),
+    ("L1 conv3x3 640", 3, 32, 640, 640),
+    ("L2 conv3x3 1280", 3, 16, 1280, 1280),
+    ("L3 conv3x3 1280", 3, 8, 1280, 1280),
+    ("L0 up conv3x3 960->320", 3, 64, 960, 320),
+    ("L0 geglu 320->2560", 1, 64, 320, 2560),
+    ("L0 ff2 1280->320", 1, 64, 1280, 320),
+    ("L0 qkv 320->960", 1, 64, 320, 960),
+    ("L0 proj 320->320", 1, 64, 320, 320),
+    ("L1 geglu 640->5120", 1, 32, 640, 5120),
+    ("L2 geglu 1280->10240", 1, 16, 1280, 10240),
+]
+
+
+def run(name, k, h, cin, cout, iters=20):
+    x = torch.randn(N, h, h, cin, device=dev, dtype=torch.float16)
+    w = torch.randn(cout, cin, k, k, device=dev) / math.sqrt(k * k * cin)
+    wp, kp = ops.pack_conv_weight(w)
+    out = torch.empty(N, h, h, cout, device=dev, dtype=torch.float16)
+    for _ in range(3):
+        ops.conv(x, wp, kp, cout, ksize=k, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        ops.conv(x, wp, kp, cout, ksize=k, out=out)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    fl = 2.0 * N * h * h * cout * k * k * cin
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w, padding=k // 2).permute(0, 2, 3, 1)
+    err = ((out.float() - ref).norm() / ref.norm()).item()
+    print(f"{name:26s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  relerr {err:.1e}", flush=True)
+
+
+for s in SHAPES:
+    run(*s)
