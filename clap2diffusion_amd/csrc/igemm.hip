@@ -110,80 +110,123 @@ __device__ __forceinline__ f16x8 apply_pro(const IgemmParams& p, f16x8 v, int n,
     return v;
 }
 
-// ---- epilogue: lane holds out[row = m-tile row (lane&15)][cols 4*(lane>>4) .. +3]
-template <int BM, int BN>
-__device__ __forceinline__ void epilogue(const IgemmParams& p, f32x4 (&acc)[BN / 32][BM / 32], int m0, int n0, int wm,
-                                         int wn, int lane) {
-    constexpr int TM = BM / 32, TN = BN / 32;
+// ---- epilogue: lane holds out[row mrow0 + 16 b + (lane&15)][cols ncol0 + 16 a + 4 (lane>>4) .. +3]
+// All operand loads (bias, temb, residual) are issued first from clamped, always
+// valid addresses, then the math, then the stores: no load waits behind a store
+// (out may alias resid for in-place residual adds; every element is read before
+// it is written by the same lane, so that stays correct).
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue_tiles(const IgemmParams& p, f32x4 (&acc)[TN][TM], int mrow0, int ncol0,
+                                               int lane) {
     const int hw = p.oh * p.ow;
-    const bool geglu = (p.act == C2D_ACT_GEGLU);
+    const int lr = lane & 15, lc = 4 * (lane >> 4);
+    int mrow[TM], nimg[TM];
+    bool mok[TM];
 #pragma unroll
     for (int b = 0; b < TM; ++b) {
-        const int m = m0 + wm * (BM / 2) + b * 16 + (lane & 15);
-        if (m >= p.M) continue;
-        const int nimg = m / hw;
-        if (!geglu) {
+        const int m = mrow0 + b * 16 + lr;
+        mok[b] = m < p.M;
+        mrow[b] = mok[b] ? m : p.M - 1;
+        nimg[b] = mrow[b] / hw;
+    }
+    if (p.act != C2D_ACT_GEGLU) {
+        int col[TN];
+        bool cok[TN];
+        float4 bv[TN];
+#pragma unroll
+        for (int a = 0; a < TN; ++a) {
+            const int j = ncol0 + a * 16 + lc;
+            cok[a] = j < p.cout;
+            col[a] = cok[a] ? j : 0;
+            bv[a] = p.bias ? *reinterpret_cast<const float4*>(p.bias + col[a]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        f16x4 rv[TM][TN], tv[TM][TN];
+        if (p.resid) {
+#pragma unroll
+            for (int b = 0; b < TM; ++b)
+#pragma unroll
+                for (int a = 0; a < TN; ++a)
+                    rv[b][a] = *reinterpret_cast<const f16x4*>(p.resid + (size_t)mrow[b] * p.resid_ld + col[a]);
+        }
+        if (p.temb) {
+#pragma unroll
+            for (int b = 0; b < TM; ++b)
+#pragma unroll
+                for (int a = 0; a < TN; ++a)
+                    tv[b][a] = *reinterpret_cast<const f16x4*>(p.temb + (size_t)nimg[b] * p.temb_ld + col[a]);
+        }
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
 #pragma unroll
             for (int a = 0; a < TN; ++a) {
-                const int j = n0 + wn * (BN / 2) + a * 16 + 4 * (lane >> 4);
-                if (j >= p.cout) continue;
-                float v[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-                if (p.bias) {
-                    float4 bb = *reinterpret_cast<const float4*>(p.bias + j);
-                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-                }
+                float v[4] = {acc[a][b][0] + bv[a].x, acc[a][b][1] + bv[a].y, acc[a][b][2] + bv[a].z,
+                              acc[a][b][3] + bv[a].w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
                     else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
                     else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
-                }
-                if (p.temb) {
-                    f16x4 t = *reinterpret_cast<const f16x4*>(p.temb + (size_t)nimg * p.temb_ld + j);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
-                }
-                if (p.resid) {
-                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                    if (p.temb) v[r] += (float)tv[b][a][r];
+                    if (p.resid) v[r] += (float)rv[b][a][r];
                 }
                 f16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
-                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+                if (mok[b] && cok[a]) *reinterpret_cast<f16x4*>(p.out + (size_t)mrow[b] * p.out_ld + col[a]) = o;
             }
-        } else {
-            // packed rows: [16 h | 16 g] per 32-row block -> 16 output features
+        }
+    } else {
+        // packed rows: [16 h | 16 g] per 32-row block -> 16 output features
+        constexpr int TP = TN / 2;
+        int jo[TP], jh[TP];
+        bool cok[TP];
+        float4 bh[TP], bg[TP];
 #pragma unroll
-            for (int a = 0; a < TN; a += 2) {
-                const int jp = n0 + wn * (BN / 2) + a * 16;  // packed row of the h block
-                if (jp >= p.cout) continue;
-                const int jo = (jp >> 1) + 4 * (lane >> 4);  // output feature
-                const int jh = jp + 4 * (lane >> 4), jg = jh + 16;
-                float hv[4] = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-                float gv[4] = {acc[a + 1][b][0], acc[a + 1][b][1], acc[a + 1][b][2], acc[a + 1][b][3]};
-                if (p.bias) {
-                    float4 bh = *reinterpret_cast<const float4*>(p.bias + jh);
-                    float4 bg = *reinterpret_cast<const float4*>(p.bias + jg);
-                    hv[0] += bh.x; hv[1] += bh.y; hv[2] += bh.z; hv[3] += bh.w;
-                    gv[0] += bg.x; gv[1] += bg.y; gv[2] += bg.z; gv[3] += bg.w;
-                }
-                float v[4];
+        for (int q = 0; q < TP; ++q) {
+            const int jp = ncol0 + 2 * q * 16;
+            cok[q] = jp < p.cout;
+            const int jpc = cok[q] ? jp : 0;
+            jo[q] = (jpc >> 1) + lc;
+            jh[q] = jpc + lc;
+            bh[q] = p.bias ? *reinterpret_cast<const float4*>(p.bias + jh[q]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            bg[q] = p.bias ? *reinterpret_cast<const float4*>(p.bias + jh[q] + 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        f16x4 rv[TM][TP];
+        if (p.resid) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = hv[r] * gelu_f(gv[r]);
-                if (p.resid) {
-                    f16x4 t = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + jo);
+            for (int b = 0; b < TM; ++b)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
-                }
+                for (int q = 0; q < TP; ++q)
+                    rv[b][q] = *reinterpret_cast<const f16x4*>(p.resid + (size_t)mrow[b] * p.resid_ld + jo[q]);
+        }
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+#pragma unroll
+            for (int q = 0; q < TP; ++q) {
+                const f32x4 h4 = acc[2 * q][b], g4 = acc[2 * q + 1][b];
+                const float hb[4] = {bh[q].x, bh[q].y, bh[q].z, bh[q].w}, gb[4] = {bg[q].x, bg[q].y, bg[q].z, bg[q].w};
                 f16x4 o;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
-                *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + jo) = o;
+                for (int r = 0; r < 4; ++r) {
+                    float v = (h4[r] + hb[r]) * gelu_f(g4[r] + gb[r]);
+                    if (p.resid) v += (float)rv[b][q][r];
+                    o[r] = (f16)v;
+                }
+                if (mok[b] && cok[q]) *reinterpret_cast<f16x4*>(p.out + (size_t)mrow[b] * p.out_ld + jo[q]) = o;
             }
         }
     }
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void epilogue(const IgemmParams& p, f32x4 (&acc)[BN / 32][BM / 32], int m0, int n0, int wm,
+                                         int wn, int lane) {
+    epilogue_tiles<BM / 32, BN / 32>(p, acc, m0 + wm * (BM / 2), n0 + wn * (BN / 2), lane);
+}
+
+// per-wave 64x64 tile epilogue
+__device__ __forceinline__ void epilogue_w64(const IgemmParams& p, f32x4 (&acc)[4][4], int mw0, int nw0, int lane) {
+    epilogue_tiles<4, 4>(p, acc, mw0, nw0, lane);
 }
 
 template <int BM, int BN, int AMODE>
@@ -371,12 +414,13 @@ __global__ void __launch_bounds__(256) igemm_glds_kernel(IgemmParams p) {
             const int c = cbase + a_c[i] * 8;
             const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
             const bool v = a_ok[i] && c < p.cin && iy >= 0 && iy < p.vh && ix >= 0 && ix < p.vw;
-            const f16* src = zero;
-            if (v) {
-                const int sy = p.up ? (iy >> 1) : iy, sx = p.up ? (ix >> 1) : ix;
-                const size_t pix = ((size_t)a_n[i] * p.h + sy) * p.w + sx;
-                src = (c < p.c0) ? (p.src0 + pix * p.c0 + c) : (p.src1 + pix * p.c1 + (c - p.c0));
-            }
+            // branchless: clamp, compute the address unconditionally, select the zero page
+            const int sy = v ? (p.up ? (iy >> 1) : iy) : 0, sx = v ? (p.up ? (ix >> 1) : ix) : 0;
+            const size_t pix = ((size_t)a_n[i] * p.h + sy) * p.w + sx;
+            const bool hi = c >= p.c0;
+            const f16* sb = hi ? p.src1 : p.src0;
+            const size_t off = pix * (size_t)(hi ? p.c1 : p.c0) + (hi ? c - p.c0 : c);
+            const f16* src = v ? sb + off : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + (wave * AI + i) * 1024), 16, 0, 0);
         }
 #pragma unroll
@@ -427,6 +471,158 @@ static void launch_glds(const IgemmParams& p, hipStream_t s) {
     hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, AMODE>), dim3(p.gx * p.gy), dim3(256), smem, s, p);
 }
 
+
+// ---------------------------------------------------------------------------
+// Multi-stage LDS-DMA pipeline: WM x WN waves, each owning a 64x64 output tile
+// (4x4 MFMA 16x16x32 tiles), BK = 64, STAGES-deep LDS ring.  Stage kt+STAGES-1
+// is issued right after the barrier that proves stage kt landed, so
+// STAGES-1 K steps of loads are in flight behind the MFMAs.  Waits are
+// counted (vmcnt = glds per stage x stages left in flight) and the barrier is
+// a raw s_barrier, so no vmcnt(0) drains the ring inside the loop.
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+    // s_waitcnt simm16 (gfx9 family): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+    switch (n) {
+        case 0: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8) | ((0 >> 4) << 14)); break;
+        case 6: __builtin_amdgcn_s_waitcnt((6 & 15) | (7 << 4) | (15 << 8) | ((6 >> 4) << 14)); break;
+        case 8: __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (15 << 8) | ((8 >> 4) << 14)); break;
+        case 12: __builtin_amdgcn_s_waitcnt((12 & 15) | (7 << 4) | (15 << 8) | ((12 >> 4) << 14)); break;
+        case 16: __builtin_amdgcn_s_waitcnt((16 & 15) | (7 << 4) | (15 << 8) | ((16 >> 4) << 14)); break;
+        case 18: __builtin_amdgcn_s_waitcnt((18 & 15) | (7 << 4) | (15 << 8) | ((18 >> 4) << 14)); break;
+        case 24: __builtin_amdgcn_s_waitcnt((24 & 15) | (7 << 4) | (15 << 8) | ((24 >> 4) << 14)); break;
+        default: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8)); break;
+    }
+}
+
+template <int WM, int WN, int STAGES, int AMODE>
+__global__ void __launch_bounds__(64 * WM * WN) igemm_pipe_kernel(IgemmParams p) {
+    constexpr int NW = WM * WN;
+    constexpr int BM = 64 * WM, BN = 64 * WN;
+    constexpr int TM = 4, TN = 4;
+    constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);   // glds per wave per stage
+    constexpr int PER = AI + BI;
+    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+    static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave mismatch");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+    const int tile = xcd_remap(blockIdx.x, p.gx * p.gy);
+    const int mt = tile / p.gx, nt = tile - mt * p.gx;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int lrow = lane >> 3, slot = lane & 7;
+    const f16* zero = c2d_zero_page;
+    const int hw = p.oh * p.ow;
+
+    int a_n[AI], a_iy[AI], a_ix[AI], a_c[AI];
+    bool a_ok[AI];
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+        const int row = (wave * AI + i) * 8 + lrow;
+        const int m = m0 + row;
+        a_ok[i] = m < p.M;
+        const int mm = a_ok[i] ? m : 0;
+        const int nn = mm / hw, r = mm - nn * hw;
+        const int oy = r / p.ow, ox = r - oy * p.ow;
+        a_n[i] = nn;
+        a_iy[i] = oy * p.stride - p.pad;
+        a_ix[i] = ox * p.stride - p.pad;
+        a_c[i] = slot ^ ((row >> 1) & 7);
+    }
+    const f16* b_src[BI];
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+        const int row = (wave * BI + i) * 8 + lrow;
+        const int j = n0 + row;
+        b_src[i] = (j < p.cout) ? p.wt + (size_t)j * p.kpad + (slot ^ ((row >> 1) & 7)) * 8 : nullptr;
+    }
+
+    auto issue = [&](int kt, int buf) {
+        const int k0 = kt * 64;
+        int ky = 0, kx = 0, cbase = k0;
+        if (AMODE == AM_3X3_FAST) {
+            const int tap = k0 / p.cin;
+            cbase = k0 - tap * p.cin;
+            ky = tap / 3;
+            kx = tap - ky * 3;
+        }
+        char* base = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+            const int c = cbase + a_c[i] * 8;
+            const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
+            const bool v = a_ok[i] && c < p.cin && iy >= 0 && iy < p.vh && ix >= 0 && ix < p.vw;
+            // branchless: clamp, compute the address unconditionally, select the zero page
+            const int sy = v ? (p.up ? (iy >> 1) : iy) : 0, sx = v ? (p.up ? (ix >> 1) : ix) : 0;
+            const size_t pix = ((size_t)a_n[i] * p.h + sy) * p.w + sx;
+            const bool hi = c >= p.c0;
+            const f16* sb = hi ? p.src1 : p.src0;
+            const size_t off = pix * (size_t)(hi ? p.c1 : p.c0) + (hi ? c - p.c0 : c);
+            const f16* src = v ? sb + off : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + (wave * AI + i) * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < BI; ++i) {
+            const f16* src = b_src[i] ? b_src[i] + k0 : zero;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + A_BYTES + (wave * BI + i) * 1024), 16, 0, 0);
+        }
+    };
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    const int nk = p.kpad / 64;
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+        if (s0 < nk) issue(s0, s0);
+    int rd = 0, wr = STAGES - 1;
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + STAGES - 2 < nk) wait_vmcnt_le(PER * (STAGES - 2));
+        else wait_vmcnt_le(0);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, wr);
+        const char* As = smem + rd * STAGE;
+        const char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int ch = kk * 4 + (lane >> 4);
+            f16x8 fa[TM], fb[TN];
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+                fa[t] = *reinterpret_cast<const f16x8*>(As + lds_off(wm * 64 + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int t = 0; t < TN; ++t)
+                fb[t] = *reinterpret_cast<const f16x8*>(Bs + lds_off(wn * 64 + t * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+        }
+        rd = (rd + 1 == STAGES) ? 0 : rd + 1;
+        wr = (wr + 1 == STAGES) ? 0 : wr + 1;
+    }
+    // epilogue indexing assumes a 2x2-style (BM/2, BN/2) split; remap to per-wave 64x64 tiles
+    epilogue_w64(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
+}
+
+template <int WM, int WN, int STAGES, int AMODE>
+static void launch_pipe(const IgemmParams& p, hipStream_t s) {
+    const int smem = STAGES * (64 * WM + 64 * WN) * 128;
+    auto k = igemm_pipe_kernel<WM, WN, STAGES, AMODE>;
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(p.gx * p.gy), dim3(64 * WM * WN), smem, s, p);
+}
+
 template <int BM, int BN, int AMODE>
 static void launch(const IgemmParams& p, hipStream_t s) {
     const int smem = 2 * (BM + BN) * 128;
@@ -438,11 +634,12 @@ static void launch(const IgemmParams& p, hipStream_t s) {
 
 using namespace c2d;
 
-// C2D_NO_GLDS=1 forces the register-staged kernel (A/B comparisons, debugging)
-static bool getenv_noglds() {
+// C2D_GEMM_MODE=1 restricts to the double-buffered glds kernels, =2 to the
+// register-staged ones (A/B comparisons, debugging); default 0 = auto.
+static int gemm_mode() {
     static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_NO_GLDS"); v = (e && e[0] == '1') ? 1 : 0; }
-    return v == 1;
+    if (v < 0) { const char* e = getenv("C2D_GEMM_MODE"); v = e ? atoi(e) : 0; }
+    return v;
 }
 
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
@@ -492,11 +689,19 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
 
     hipStream_t s = (hipStream_t)stream;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
-    const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !getenv_noglds();
-    // small problems: 64x64 tiles to fill 256 CUs
-    const long tiles128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
-    const bool small = tiles128 < 512;
-    if (small) {
+    const int mode = gemm_mode();  // 0 auto, 1 double-buffer glds only, 2 register-staged only
+    const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && mode != 2;
+    const long t256 = (long)((p.M + 255) / 256) * ((d->cout + 127) / 128);
+    const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
+    if (dma && mode == 0 && d->cout >= 128 && t256 >= 384) {
+        p.gx = (d->cout + 127) / 128; p.gy = (p.M + 255) / 256;
+        if (amode == AM_1X1) launch_pipe<4, 2, 3, AM_1X1>(p, s);
+        else launch_pipe<4, 2, 3, AM_3X3_FAST>(p, s);
+    } else if (dma && mode == 0 && d->cout >= 128 && t128 >= 256) {
+        p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
+        if (amode == AM_1X1) launch_pipe<2, 2, 4, AM_1X1>(p, s);
+        else launch_pipe<2, 2, 4, AM_3X3_FAST>(p, s);
+    } else if (t128 < 512) {
         p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
         if (dma) {
             if (amode == AM_1X1) launch_glds<64, 64, AM_1X1>(p, s);
