@@ -24,7 +24,7 @@ EXPORTS = [
     "c2d_conv2d_igemm", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_layernorm_stats",
     "c2d_layernorm", "c2d_attention_fwd", "c2d_window_attention", "c2d_htsat_mel_patches",
     "c2d_patch_merge_gather", "c2d_row_mean", "c2d_l2_normalize", "c2d_timestep_embedding",
-    "c2d_cfg_ddim_step", "c2d_latent_to_nhwc", "c2d_add", "c2d_last_hip_error", "c2d_version",
+    "c2d_cfg_ddim_step", "c2d_latent_to_nhwc", "c2d_upsample_nearest2x", "c2d_add", "c2d_last_hip_error", "c2d_version",
 ]
 
 
@@ -70,6 +70,7 @@ def lib() -> ctypes.CDLL:
         "c2d_timestep_embedding": ([vp, vp, i, i, vp, vp], i),
         "c2d_cfg_ddim_step": ([vp, vp, i, i, i, f, vp, vp, i, vp], i),
         "c2d_latent_to_nhwc": ([vp, i, i, i, i, i, vp, vp], i),
+        "c2d_upsample_nearest2x": ([vp, i, i, i, i, vp, vp], i),
         "c2d_add": ([vp, vp, vp, sz, vp], i),
         "c2d_last_hip_error": ([], i),
         "c2d_version": ([], ctypes.c_char_p),

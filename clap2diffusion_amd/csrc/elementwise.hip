@@ -172,6 +172,31 @@ extern "C" int c2d_latent_to_nhwc(const float* x, int n, int c, int hw, int cpad
     return check_launch();
 }
 
+__global__ void upsample2x_kernel(const f16x8* __restrict__ x, int h, int w, int c8, f16x8* __restrict__ out,
+                                  size_t total) {
+    // one thread per output 16-byte chunk; consecutive threads walk channels then columns
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int cc = (int)(i % c8);
+        const size_t pix = i / c8;
+        const int ox = (int)(pix % (2 * w));
+        const size_t r = pix / (2 * w);
+        const int oy = (int)(r % (2 * h));
+        const size_t n = r / (2 * h);
+        out[i] = x[((n * h + (oy >> 1)) * w + (ox >> 1)) * c8 + cc];
+    }
+}
+
+extern "C" int c2d_upsample_nearest2x(const void* x, int n, int h, int w, int c, void* out, void* stream) {
+    if (!x || !out) return C2D_E_ARG;
+    if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || (c & 7)) return C2D_E_SHAPE;
+    if (!aligned16(x) || !aligned16(out)) return C2D_E_ALIGN;
+    const size_t total = (size_t)n * 4 * h * w * (c / 8);
+    const unsigned blocks = (unsigned)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(upsample2x_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const f16x8*)x, h, w, c / 8,
+                       (f16x8*)out, total);
+    return check_launch();
+}
+
 extern "C" int c2d_add(const void* a, const void* b, void* out, size_t n, void* stream) {
     if (!a || !b || !out) return C2D_E_ARG;
     if (n & 7) return C2D_E_SHAPE;

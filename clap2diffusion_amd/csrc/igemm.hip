@@ -347,158 +347,47 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgemmParams p) {
 
 
 // ---------------------------------------------------------------------------
-// LDS-DMA pipeline (no prologue): A and B tiles go HBM -> LDS with
-// global_load_lds_dwordx4 (16 B per lane, one 1-KiB wave instruction per 8 rows),
-// double-buffered, so the next K step streams in while this one runs on MFMA,
-// with no staging VGPRs and no ds_write.  The LDS image is lane-linear, so the
-// XOR bank swizzle is applied to the per-lane SOURCE chunk (lane slot s of row r
-// fetches logical chunk s ^ f(r)) and undone on the read (lds_off).  Padding /
-// out-of-range lanes fetch from a zero page, so halo and tails need no masking.
+// LDS-DMA implicit-GEMM kernels (no prologue).
+//
+// A and B tiles go HBM -> LDS with global_load_lds_dwordx4 (16 B per lane, one
+// 1-KiB wave instruction per 8 tile rows) into a STAGES-deep ring; stage kt+S-1
+// is issued right after the barrier that proves stage kt landed, so S-1 K steps
+// of loads are in flight behind the MFMAs.  Waits are counted (vmcnt = glds per
+// stage x stages left in flight) and the barrier is a raw s_barrier, so nothing
+// drains the ring inside the loop.  The LDS image is lane-linear: the XOR bank
+// swizzle goes on the per-lane SOURCE chunk (slot s of row r fetches logical
+// chunk s ^ f(r)) and is undone on the read (lds_off).
+//
+// Addressing is precomputed per staged row: the element offset of (pixel, chunk)
+// for each source and a 9-bit in-bounds mask over the 3x3 taps, so a K step
+// costs one scalar tap/source decision plus ~7 VALU per DMA instruction; invalid
+// lanes (halo, tails) fetch from a zero page.  Requires c0 % 64 == 0 when two
+// sources are used (a 64-wide K step never straddles the concat seam) and no
+// nearest-x2 view (the UNet materialises the upsample instead).
 __device__ __attribute__((aligned(64))) f16 c2d_zero_page[64];
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-template <int BM, int BN, int AMODE>
-__global__ void __launch_bounds__(256) igemm_glds_kernel(IgemmParams p) {
-    constexpr int TM = BM / 32, TN = BN / 32;
-    constexpr int AI = BM / 32, BI = BN / 32;        // glds instructions per wave per K step
-    constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int tile = xcd_remap(blockIdx.x, p.gx * p.gy);
-    const int mt = tile / p.gx, nt = tile - mt * p.gx;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int lrow = lane >> 3, slot = lane & 7;
-    const f16* zero = c2d_zero_page;
-    const int hw = p.oh * p.ow;
-
-    int a_n[AI], a_iy[AI], a_ix[AI], a_c[AI];
-    bool a_ok[AI];
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-        const int row = (wave * AI + i) * 8 + lrow;
-        const int m = m0 + row;
-        a_ok[i] = m < p.M;
-        const int mm = a_ok[i] ? m : 0;
-        const int nn = mm / hw, r = mm - nn * hw;
-        const int oy = r / p.ow, ox = r - oy * p.ow;
-        a_n[i] = nn;
-        a_iy[i] = oy * p.stride - p.pad;
-        a_ix[i] = ox * p.stride - p.pad;
-        a_c[i] = slot ^ ((row >> 1) & 7);
-    }
-    const f16* b_src[BI];
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-        const int row = (wave * BI + i) * 8 + lrow;
-        const int j = n0 + row;
-        b_src[i] = (j < p.cout) ? p.wt + (size_t)j * p.kpad + (slot ^ ((row >> 1) & 7)) * 8 : nullptr;
-    }
-
-    auto issue = [&](int kt, int buf) {
-        const int k0 = kt * 64;
-        int ky = 0, kx = 0, cbase = k0;
-        if (AMODE == AM_3X3_FAST) {
-            const int tap = k0 / p.cin;
-            cbase = k0 - tap * p.cin;
-            ky = tap / 3;
-            kx = tap - ky * 3;
-        }
-        char* base = smem + buf * STAGE;
-#pragma unroll
-        for (int i = 0; i < AI; ++i) {
-            const int c = cbase + a_c[i] * 8;
-            const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
-            const bool v = a_ok[i] && c < p.cin && iy >= 0 && iy < p.vh && ix >= 0 && ix < p.vw;
-            // branchless: clamp, compute the address unconditionally, select the zero page
-            const int sy = v ? (p.up ? (iy >> 1) : iy) : 0, sx = v ? (p.up ? (ix >> 1) : ix) : 0;
-            const size_t pix = ((size_t)a_n[i] * p.h + sy) * p.w + sx;
-            const bool hi = c >= p.c0;
-            const f16* sb = hi ? p.src1 : p.src0;
-            const size_t off = pix * (size_t)(hi ? p.c1 : p.c0) + (hi ? c - p.c0 : c);
-            const f16* src = v ? sb + off : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + (wave * AI + i) * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < BI; ++i) {
-            const f16* src = b_src[i] ? b_src[i] + k0 : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + A_BYTES + (wave * BI + i) * 1024), 16, 0, 0);
-        }
-    };
-
-    f32x4 acc[TN][TM];
-#pragma unroll
-    for (int a = 0; a < TN; ++a)
-#pragma unroll
-        for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    const int nk = p.kpad / 64;
-    issue(0, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // stage kt landed for every wave; every wave is done reading stage kt-1
-        if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-        const char* As = smem + buf * STAGE;
-        const char* Bs = As + A_BYTES;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int ch = kk * 4 + (lane >> 4);
-            f16x8 fa[TM], fb[TN];
-#pragma unroll
-            for (int t = 0; t < TM; ++t)
-                fa[t] = *reinterpret_cast<const f16x8*>(As + lds_off(wm * (BM / 2) + t * 16 + (lane & 15), ch));
-#pragma unroll
-            for (int t = 0; t < TN; ++t)
-                fb[t] = *reinterpret_cast<const f16x8*>(Bs + lds_off(wn * (BN / 2) + t * 16 + (lane & 15), ch));
-#pragma unroll
-            for (int a = 0; a < TN; ++a)
-#pragma unroll
-                for (int b = 0; b < TM; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
-        }
-    }
-    epilogue<BM, BN>(p, acc, m0, n0, wm, wn, lane);
-}
-
-template <int BM, int BN, int AMODE>
-static void launch_glds(const IgemmParams& p, hipStream_t s) {
-    const int smem = 2 * (BM + BN) * 128;
-    hipLaunchKernelGGL((igemm_glds_kernel<BM, BN, AMODE>), dim3(p.gx * p.gy), dim3(256), smem, s, p);
-}
-
-
-// ---------------------------------------------------------------------------
-// Multi-stage LDS-DMA pipeline: WM x WN waves, each owning a 64x64 output tile
-// (4x4 MFMA 16x16x32 tiles), BK = 64, STAGES-deep LDS ring.  Stage kt+STAGES-1
-// is issued right after the barrier that proves stage kt landed, so
-// STAGES-1 K steps of loads are in flight behind the MFMAs.  Waits are
-// counted (vmcnt = glds per stage x stages left in flight) and the barrier is
-// a raw s_barrier, so no vmcnt(0) drains the ring inside the loop.
 __device__ __forceinline__ void wait_vmcnt_le(int n) {
     // s_waitcnt simm16 (gfx9 family): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+#define C2D_WAITVM(N) __builtin_amdgcn_s_waitcnt(((N) & 15) | (7 << 4) | (15 << 8) | (((N) >> 4) << 14))
     switch (n) {
-        case 0: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8) | ((0 >> 4) << 14)); break;
-        case 6: __builtin_amdgcn_s_waitcnt((6 & 15) | (7 << 4) | (15 << 8) | ((6 >> 4) << 14)); break;
-        case 8: __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (15 << 8) | ((8 >> 4) << 14)); break;
-        case 12: __builtin_amdgcn_s_waitcnt((12 & 15) | (7 << 4) | (15 << 8) | ((12 >> 4) << 14)); break;
-        case 16: __builtin_amdgcn_s_waitcnt((16 & 15) | (7 << 4) | (15 << 8) | ((16 >> 4) << 14)); break;
-        case 18: __builtin_amdgcn_s_waitcnt((18 & 15) | (7 << 4) | (15 << 8) | ((18 >> 4) << 14)); break;
-        case 24: __builtin_amdgcn_s_waitcnt((24 & 15) | (7 << 4) | (15 << 8) | ((24 >> 4) << 14)); break;
-        default: __builtin_amdgcn_s_waitcnt((0 & 15) | (7 << 4) | (15 << 8)); break;
+        case 4: C2D_WAITVM(4); break;
+        case 6: C2D_WAITVM(6); break;
+        case 8: C2D_WAITVM(8); break;
+        case 12: C2D_WAITVM(12); break;
+        case 16: C2D_WAITVM(16); break;
+        default: C2D_WAITVM(0); break;
     }
+#undef C2D_WAITVM
 }
 
-template <int WM, int WN, int STAGES, int AMODE>
-__global__ void __launch_bounds__(64 * WM * WN) igemm_pipe_kernel(IgemmParams p) {
+template <int WM, int WN, int WT, int STAGES, int KS>
+__global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) {
     constexpr int NW = WM * WN;
-    constexpr int BM = 64 * WM, BN = 64 * WN;
-    constexpr int TM = 4, TN = 4;
-    constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);   // glds per wave per stage
+    constexpr int BM = WM * WT * 16, BN = WN * WT * 16;
+    constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);   // DMA instructions per wave per stage
     constexpr int PER = AI + BI;
     constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
     static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave mismatch");
@@ -514,20 +403,30 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pipe_kernel(IgemmParams p)
     const f16* zero = c2d_zero_page;
     const int hw = p.oh * p.ow;
 
-    int a_n[AI], a_iy[AI], a_ix[AI], a_c[AI];
-    bool a_ok[AI];
+    // ---- per staged A row: element offsets in each source + tap mask
+    int a_off0[AI], a_off1[AI], a_ch[AI];
+    unsigned a_mask[AI];
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
         const int row = (wave * AI + i) * 8 + lrow;
         const int m = m0 + row;
-        a_ok[i] = m < p.M;
-        const int mm = a_ok[i] ? m : 0;
+        const int mm = m < p.M ? m : 0;
         const int nn = mm / hw, r = mm - nn * hw;
         const int oy = r / p.ow, ox = r - oy * p.ow;
-        a_n[i] = nn;
-        a_iy[i] = oy * p.stride - p.pad;
-        a_ix[i] = ox * p.stride - p.pad;
-        a_c[i] = slot ^ ((row >> 1) & 7);
+        const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+        unsigned mask = 0;
+        if (m < p.M) {
+#pragma unroll
+            for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < KS; ++kx)
+                    if (iy0 + ky >= 0 && iy0 + ky < p.h && ix0 + kx >= 0 && ix0 + kx < p.w) mask |= 1u << (ky * KS + kx);
+        }
+        const int pix0 = (nn * p.h + iy0) * p.w + ix0;
+        a_ch[i] = (slot ^ ((row >> 1) & 7)) * 8;
+        a_off0[i] = pix0 * p.c0 + a_ch[i];
+        a_off1[i] = pix0 * p.c1 + a_ch[i];
+        a_mask[i] = mask;
     }
     const f16* b_src[BI];
 #pragma unroll
@@ -539,25 +438,18 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pipe_kernel(IgemmParams p)
 
     auto issue = [&](int kt, int buf) {
         const int k0 = kt * 64;
-        int ky = 0, kx = 0, cbase = k0;
-        if (AMODE == AM_3X3_FAST) {
-            const int tap = k0 / p.cin;
-            cbase = k0 - tap * p.cin;
-            ky = tap / 3;
-            kx = tap - ky * 3;
-        }
+        const int tap = (KS == 3) ? k0 / p.cin : 0;              // uniform
+        const int cbase = k0 - tap * p.cin;
+        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+        const bool use1 = cbase >= p.c0;
+        const f16* sb = use1 ? p.src1 : p.src0;
+        const int cs = use1 ? p.c1 : p.c0;
+        const int sterm = (KS == 3 ? (ky * p.w + kx) * cs : 0) + (use1 ? cbase - p.c0 : cbase);
         char* base = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < AI; ++i) {
-            const int c = cbase + a_c[i] * 8;
-            const int iy = a_iy[i] + ky, ix = a_ix[i] + kx;
-            const bool v = a_ok[i] && c < p.cin && iy >= 0 && iy < p.vh && ix >= 0 && ix < p.vw;
-            // branchless: clamp, compute the address unconditionally, select the zero page
-            const int sy = v ? (p.up ? (iy >> 1) : iy) : 0, sx = v ? (p.up ? (ix >> 1) : ix) : 0;
-            const size_t pix = ((size_t)a_n[i] * p.h + sy) * p.w + sx;
-            const bool hi = c >= p.c0;
-            const f16* sb = hi ? p.src1 : p.src0;
-            const size_t off = pix * (size_t)(hi ? p.c1 : p.c0) + (hi ? c - p.c0 : c);
+            const bool v = ((a_mask[i] >> tap) & 1u) && (cbase + a_ch[i] < p.cin);
+            const int off = (use1 ? a_off1[i] : a_off0[i]) + sterm;
             const f16* src = v ? sb + off : zero;
             __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + (wave * AI + i) * 1024), 16, 0, 0);
         }
@@ -568,11 +460,23 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pipe_kernel(IgemmParams p)
         }
     };
 
-    f32x4 acc[TN][TM];
+    // ---- fragment read offsets (loop invariant)
+    int fa_off[2][WT], fb_off[2][WT];
 #pragma unroll
-    for (int a = 0; a < TN; ++a)
+    for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
 #pragma unroll
-        for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < WT; ++t) {
+            fa_off[kk][t] = lds_off(wm * WT * 16 + t * 16 + (lane & 15), ch);
+            fb_off[kk][t] = A_BYTES + lds_off(wn * WT * 16 + t * 16 + (lane & 15), ch);
+        }
+    }
+
+    f32x4 acc[WT][WT];
+#pragma unroll
+    for (int a = 0; a < WT; ++a)
+#pragma unroll
+        for (int b = 0; b < WT; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const int nk = p.kpad / 64;
 #pragma unroll
@@ -586,35 +490,30 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pipe_kernel(IgemmParams p)
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, wr);
-        const char* As = smem + rd * STAGE;
-        const char* Bs = As + A_BYTES;
+        const char* S = smem + rd * STAGE;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            const int ch = kk * 4 + (lane >> 4);
-            f16x8 fa[TM], fb[TN];
+            f16x8 fa[WT], fb[WT];
 #pragma unroll
-            for (int t = 0; t < TM; ++t)
-                fa[t] = *reinterpret_cast<const f16x8*>(As + lds_off(wm * 64 + t * 16 + (lane & 15), ch));
+            for (int t = 0; t < WT; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + fa_off[kk][t]);
 #pragma unroll
-            for (int t = 0; t < TN; ++t)
-                fb[t] = *reinterpret_cast<const f16x8*>(Bs + lds_off(wn * 64 + t * 16 + (lane & 15), ch));
+            for (int t = 0; t < WT; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + fb_off[kk][t]);
 #pragma unroll
-            for (int a = 0; a < TN; ++a)
+            for (int a = 0; a < WT; ++a)
 #pragma unroll
-                for (int b = 0; b < TM; ++b)
+                for (int b = 0; b < WT; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
         }
         rd = (rd + 1 == STAGES) ? 0 : rd + 1;
         wr = (wr + 1 == STAGES) ? 0 : wr + 1;
     }
-    // epilogue indexing assumes a 2x2-style (BM/2, BN/2) split; remap to per-wave 64x64 tiles
-    epilogue_w64(p, acc, m0 + wm * 64, n0 + wn * 64, lane);
+    epilogue_tiles<WT, WT>(p, acc, m0 + wm * WT * 16, n0 + wn * WT * 16, lane);
 }
 
-template <int WM, int WN, int STAGES, int AMODE>
-static void launch_pipe(const IgemmParams& p, hipStream_t s) {
-    const int smem = STAGES * (64 * WM + 64 * WN) * 128;
-    auto k = igemm_pipe_kernel<WM, WN, STAGES, AMODE>;
+template <int WM, int WN, int WT, int STAGES, int KS>
+static void launch_dma(const IgemmParams& p, hipStream_t s) {
+    constexpr int smem = STAGES * (WM + WN) * WT * 16 * 128;
+    auto k = igemm_dma_kernel<WM, WN, WT, STAGES, KS>;
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -634,8 +533,8 @@ static void launch(const IgemmParams& p, hipStream_t s) {
 
 using namespace c2d;
 
-// C2D_GEMM_MODE=1 restricts to the double-buffered glds kernels, =2 to the
-// register-staged ones (A/B comparisons, debugging); default 0 = auto.
+// C2D_GEMM_MODE=2 restricts to the register-staged kernels (A/B comparisons,
+// debugging); default 0 = auto.
 static int gemm_mode() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_GEMM_MODE"); v = e ? atoi(e) : 0; }
@@ -689,32 +588,30 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
 
     hipStream_t s = (hipStream_t)stream;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
-    const int mode = gemm_mode();  // 0 auto, 1 double-buffer glds only, 2 register-staged only
-    const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && mode != 2;
+    const int mode = gemm_mode();  // 0 auto, 2 register-staged only
+    const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && mode != 2 &&
+                     (d->c1 == 0 || (d->c0 & 63) == 0);
     const long t256 = (long)((p.M + 255) / 256) * ((d->cout + 127) / 128);
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
-    if (dma && mode == 0 && d->cout >= 128 && t256 >= 384) {
-        p.gx = (d->cout + 127) / 128; p.gy = (p.M + 255) / 256;
-        if (amode == AM_1X1) launch_pipe<4, 2, 3, AM_1X1>(p, s);
-        else launch_pipe<4, 2, 3, AM_3X3_FAST>(p, s);
-    } else if (dma && mode == 0 && d->cout >= 128 && t128 >= 256) {
-        p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
-        if (amode == AM_1X1) launch_pipe<2, 2, 4, AM_1X1>(p, s);
-        else launch_pipe<2, 2, 4, AM_3X3_FAST>(p, s);
+    if (dma) {
+        if (d->cout >= 128 && t256 >= 384) {
+            p.gx = (d->cout + 127) / 128; p.gy = (p.M + 255) / 256;
+            if (d->ksize == 1) launch_dma<4, 2, 4, 3, 1>(p, s); else launch_dma<4, 2, 4, 3, 3>(p, s);
+        } else if (d->cout >= 128 && t128 >= 256) {
+            p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
+            if (d->ksize == 1) launch_dma<2, 2, 4, 3, 1>(p, s); else launch_dma<2, 2, 4, 3, 3>(p, s);
+        } else {
+            p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
+            if (d->ksize == 1) launch_dma<2, 2, 2, 3, 1>(p, s); else launch_dma<2, 2, 2, 3, 3>(p, s);
+        }
     } else if (t128 < 512) {
         p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
-        if (dma) {
-            if (amode == AM_1X1) launch_glds<64, 64, AM_1X1>(p, s);
-            else launch_glds<64, 64, AM_3X3_FAST>(p, s);
-        } else if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);
+        if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);
         else if (amode == AM_3X3_FAST) launch<64, 64, AM_3X3_FAST>(p, s);
         else launch<64, 64, AM_3X3_GEN>(p, s);
     } else {
         p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
-        if (dma) {
-            if (amode == AM_1X1) launch_glds<128, 128, AM_1X1>(p, s);
-            else launch_glds<128, 128, AM_3X3_FAST>(p, s);
-        } else if (amode == AM_1X1) launch<128, 128, AM_1X1>(p, s);
+        if (amode == AM_1X1) launch<128, 128, AM_1X1>(p, s);
         else if (amode == AM_3X3_FAST) launch<128, 128, AM_3X3_FAST>(p, s);
         else launch<128, 128, AM_3X3_GEN>(p, s);
     }

@@ -245,6 +245,16 @@ def latent_to_nhwc(x: torch.Tensor, cpad: int, dup: bool) -> torch.Tensor:
     return out
 
 
+def upsample_nearest2x(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """NHWC fp16 nearest x2 (diffusers Upsample2D interpolate step)."""
+    n, h, w, c = x.shape
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty(n, 2 * h, 2 * w, c, device=x.device, dtype=x.dtype)
+    check(lib().c2d_upsample_nearest2x(ptr(x), n, h, w, c, ptr(out), stream_ptr()), "c2d_upsample_nearest2x")
+    return out
+
+
 def add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     if out is None:
         out = torch.empty_like(a)

@@ -197,7 +197,8 @@ class Upsample2D(nn.Module):
         self.conv = HConv2d(c, c, 3)
 
     def forward(self, x):
-        return self.conv(x, up=True)
+        # materialised x2 (one HBM pass) keeps the conv on the LDS-DMA path
+        return self.conv(ops.upsample_nearest2x(x))
 
 
 class _Block(nn.Module):

@@ -205,6 +205,11 @@ int c2d_cfg_ddim_step(const void* eps, float* x, int b, int c, int hw, float gui
 int c2d_latent_to_nhwc(const float* x, int n, int c, int hw, int cpad, int dup, void* out,
                        void* stream);
 
+/* Nearest-neighbour x2 upsample of NHWC fp16 [n, h, w, c] -> [n, 2h, 2w, c], c % 8 == 0.
+ * Replaces F.interpolate(scale_factor=2.0, mode="nearest") in diffusers Upsample2D
+ * (the UNet up path and the VAE decoder). */
+int c2d_upsample_nearest2x(const void* x, int n, int h, int w, int c, void* out, void* stream);
+
 /* out = a + b (fp16, same shape, n elements, multiple of 8). */
 int c2d_add(const void* a, const void* b, void* out, size_t n, void* stream);
 

@@ -44,6 +44,8 @@ def nchw(x):
     (2, 8, 640, 640, 1, True),
     (3, 8, 1280, 1280, 1, False),
     (16, 64, 320, 320, 1, False),
+    (16, 32, 640, 640, 1, False),
+    (4, 32, 192, 320, 1, False),
 ])
 def test_conv3x3(dev, n, h, cin, cout, stride, up):
     x = gen(n, cin, h, h, seed=1)
@@ -71,6 +73,31 @@ def test_conv3x3_gn_silu_temb_resid(dev):
     out = ops.conv(xd, wp.to(dev), kp, cout, ksize=3, bias=b.float().to(dev), gn=(sc, sh), gn_silu=True,
                    temb=temb.half().to(dev), resid=nhwc(resid).half().to(dev))
     close(nchw(out), ref)
+
+
+@pytest.mark.parametrize("n,h,c0,c1,cout,k", [
+    (2, 8, 1280, 640, 640, 3),      # 64x64 DMA tiles
+    (16, 32, 640, 320, 320, 3),     # 128x128 DMA tiles
+    (16, 64, 320, 640, 320, 3),     # 256x128 DMA tiles
+    (16, 64, 640, 320, 320, 1),     # shortcut 1x1 on the concat
+    (2, 16, 96, 32, 128, 3),        # seam not 64-aligned -> register-staged kernel
+])
+def test_conv_dual_source_plain(dev, n, h, c0, c1, cout, k):
+    x0, x1 = gen(n, c0, h, h, seed=31), gen(n, c1, h, h, seed=32)
+    w = gen(cout, c0 + c1, k, k, seed=33, scale=1.0 / math.sqrt(k * k * (c0 + c1)))
+    b = gen(cout, seed=34)
+    ref = F.conv2d(torch.cat([x0, x1], 1), w, b, padding=k // 2)
+    wp, kp = ops.pack_conv_weight(w)
+    out = ops.conv(nhwc(x0).half().to(dev), wp.to(dev), kp, cout, ksize=k, bias=b.float().to(dev),
+                   x2=nhwc(x1).half().to(dev))
+    close(nchw(out), ref)
+
+
+def test_upsample_nearest2x(dev):
+    x = gen(3, 40, 5, 7, seed=35)
+    ref = F.interpolate(x, scale_factor=2.0, mode="nearest")
+    out = ops.upsample_nearest2x(nhwc(x).half().to(dev))
+    assert torch.equal(nchw(out).cpu(), ref.half())
 
 
 def test_conv_dual_source_gn(dev):
