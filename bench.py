@@ -64,7 +64,7 @@ def measure_dominant_kernel(dev, iters: int = 20):
     tflops = flop / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
-            "kernel": "igemm_kernel<128,128,3x3> conv 320->320 @ N16x64x64",
+            "kernel": "igemm_dma_kernel<4,2,4,3,3> (256x128 tile) conv 320->320 @ N16x64x64",
             "flop_per_launch": flop, "avg_us": round(ms * 1e3, 2)}
 
 

@@ -61,6 +61,13 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    # a kernel whose host stub was silently dropped leaves an undefined c2d:: symbol
+    # that only dlopen reports; fail the build instead
+    nm = subprocess.run(["nm", "-C", "--undefined-only", str(tmp)], capture_output=True, text=True)
+    bad = [ln.strip() for ln in nm.stdout.splitlines() if "c2d::" in ln and ln.split()[0] == "U"]
+    if bad:
+        tmp.unlink()
+        raise RuntimeError("undefined device-kernel stubs in libc2d_hip.so:\n  " + "\n  ".join(bad))
     os.replace(tmp, LIB)
     stamp.write_text(dig)
     if verbose:

@@ -349,25 +349,26 @@ __global__ void __launch_bounds__(256) igemm_kernel(IgemmParams p) {
 // ---------------------------------------------------------------------------
 // LDS-DMA implicit-GEMM kernels (no prologue).
 //
-// A and B tiles go HBM -> LDS with global_load_lds_dwordx4 (16 B per lane, one
-// 1-KiB wave instruction per 8 tile rows) into a STAGES-deep ring; stage kt+S-1
-// is issued right after the barrier that proves stage kt landed, so S-1 K steps
-// of loads are in flight behind the MFMAs.  Waits are counted (vmcnt = glds per
-// stage x stages left in flight) and the barrier is a raw s_barrier, so nothing
-// drains the ring inside the loop.  The LDS image is lane-linear: the XOR bank
-// swizzle goes on the per-lane SOURCE chunk (slot s of row r fetches logical
-// chunk s ^ f(r)) and is undone on the read (lds_off).
+// A and B tiles go HBM -> LDS with buffer_load_dwordx4 ... lds (16 B per lane,
+// one 1-KiB wave instruction per 8 tile rows) into a STAGES-deep ring; stage
+// kt+S-1 is issued right after the barrier that proves stage kt landed, so S-1
+// K steps of loads are in flight behind the MFMAs.  Waits are counted (vmcnt =
+// pieces per stage x stages left in flight) and the barrier is a raw s_barrier,
+// so nothing drains the ring inside the loop.  The LDS image is lane-linear: the
+// XOR bank swizzle goes on the per-lane SOURCE chunk (slot s of row r fetches
+// logical chunk s ^ f(r)) and is undone on the read (lds_off).
 //
-// Addressing is precomputed per staged row: the element offset of (pixel, chunk)
-// for each source and a 9-bit in-bounds mask over the 3x3 taps, so a K step
-// costs one scalar tap/source decision plus ~7 VALU per DMA instruction; invalid
-// lanes (halo, tails) fetch from a zero page.  Requires c0 % 64 == 0 when two
-// sources are used (a 64-wide K step never straddles the concat seam) and no
-// nearest-x2 view (the UNet materialises the upsample instead).
-__device__ __attribute__((aligned(64))) f16 c2d_zero_page[64];
-
-typedef const __attribute__((address_space(1))) void* gptr_t;
+// Addressing: every K step is one (tap, channel block) pair, so the per-step
+// part of the source address (tap displacement, channel base, which concat
+// source) is wave-uniform and goes into the buffer descriptor's base; the lane
+// keeps a precomputed 32-bit byte offset per staged row and a 9-bit in-bounds
+// mask over the 3x3 taps.  Halo / tail lanes get an offset past num_records, and
+// the buffer unit's range check returns zeros for them -- no zero page, no
+// 64-bit address math.  Weight rows past cout are likewise out of range.
+// Requires c0 % 64 == 0 when two sources are used (a 64-wide K step never
+// straddles the concat seam) and no nearest-x2 view.
 typedef __attribute__((address_space(3))) void* lptr_t;
+constexpr unsigned kOOB = 0x80000000u;
 
 __device__ __forceinline__ void wait_vmcnt_le(int n) {
     // s_waitcnt simm16 (gfx9 family): vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
@@ -383,11 +384,37 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 #undef C2D_WAITVM
 }
 
-template <int WM, int WN, int WT, int STAGES, int KS>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+// one 1-KiB DMA piece: lane l's 16 bytes at rsrc.base + off land at lds + 16 l
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t r, char* lds, unsigned off) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lptr_t)lds, 16, off, 0, 0, 0);
+}
+
+// TM x TN 16x16 tiles of a per-wave accumulator, written in row chunks of <= 4
+// tiles so the hoisted epilogue operands stay within the register budget.
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue_chunked(const IgemmParams& p, f32x4 (&acc)[TN][TM], int mrow0, int ncol0,
+                                                 int lane) {
+    constexpr int MC = TM < 4 ? TM : 4;
+#pragma unroll
+    for (int b0 = 0; b0 < TM; b0 += MC) {
+        f32x4 sub[TN][MC];
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+            for (int b = 0; b < MC; ++b) sub[a][b] = acc[a][b0 + b];
+        epilogue_tiles<MC, TN>(p, sub, mrow0 + b0 * 16, ncol0, lane);
+    }
+}
+
+template <int WM, int WN, int TM, int TN, int STAGES, int KS>
 __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) {
     constexpr int NW = WM * WN;
-    constexpr int BM = WM * WT * 16, BN = WN * WT * 16;
-    constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);   // DMA instructions per wave per stage
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);   // DMA pieces per wave per stage
     constexpr int PER = AI + BI;
     constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
     static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave mismatch");
@@ -400,12 +427,13 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     const int mt = tile / p.gx, nt = tile - mt * p.gx;
     const int m0 = mt * BM, n0 = nt * BN;
     const int lrow = lane >> 3, slot = lane & 7;
-    const f16* zero = c2d_zero_page;
     const int hw = p.oh * p.ow;
+    const bool two = p.c1 > 0;
+    const int pshift = KS == 3 ? p.w + 1 : 0;
 
-    // ---- per staged A row: element offsets in each source + tap mask
-    int a_off0[AI], a_off1[AI], a_ch[AI];
-    unsigned a_mask[AI];
+    // ---- per staged A row: byte offsets in each source + tap mask
+    unsigned a_off0[AI], a_off1[AI], a_mask[AI];
+    int a_ch[AI];
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
         const int row = (wave * AI + i) * 8 + lrow;
@@ -422,61 +450,69 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
                 for (int kx = 0; kx < KS; ++kx)
                     if (iy0 + ky >= 0 && iy0 + ky < p.h && ix0 + kx >= 0 && ix0 + kx < p.w) mask |= 1u << (ky * KS + kx);
         }
-        const int pix0 = (nn * p.h + iy0) * p.w + ix0;
+        // window origin, biased by pshift pixels so every offset is >= 0 (the halo
+        // origin of the first pixel is -(w+1)); the descriptor base is biased back
+        const int pix0 = (nn * p.h + iy0) * p.w + ix0 + pshift;
         a_ch[i] = (slot ^ ((row >> 1) & 7)) * 8;
-        a_off0[i] = pix0 * p.c0 + a_ch[i];
-        a_off1[i] = pix0 * p.c1 + a_ch[i];
+        a_off0[i] = (unsigned)(2 * (pix0 * p.c0 + a_ch[i]));
+        a_off1[i] = (unsigned)(2 * (pix0 * p.c1 + a_ch[i]));
         a_mask[i] = mask;
     }
-    const f16* b_src[BI];
+    unsigned b_off[BI];
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
         const int row = (wave * BI + i) * 8 + lrow;
         const int j = n0 + row;
-        b_src[i] = (j < p.cout) ? p.wt + (size_t)j * p.kpad + (slot ^ ((row >> 1) & 7)) * 8 : nullptr;
+        b_off[i] = (j < p.cout) ? (unsigned)(2 * (j * p.kpad + (slot ^ ((row >> 1) & 7)) * 8)) : kOOB;
     }
+    const size_t npix = (size_t)p.n * p.h * p.w;
+    const unsigned bytes0 = (unsigned)(npix * p.c0 * 2), bytes1 = (unsigned)(npix * p.c1 * 2);
+    const unsigned wbytes = (unsigned)((size_t)p.cout * p.kpad * 2);
+    const bool ctail = (p.cin & 63) != 0;
 
+    int tap = 0, cbase = 0;                                       // (tap, channel block) of the next issue
     auto issue = [&](int kt, int buf) {
         const int k0 = kt * 64;
-        const int tap = (KS == 3) ? k0 / p.cin : 0;              // uniform
-        const int cbase = k0 - tap * p.cin;
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
-        const bool use1 = cbase >= p.c0;
-        const f16* sb = use1 ? p.src1 : p.src0;
+        const bool use1 = two && cbase >= p.c0;
         const int cs = use1 ? p.c1 : p.c0;
-        const int sterm = (KS == 3 ? (ky * p.w + kx) * cs : 0) + (use1 ? cbase - p.c0 : cbase);
+        const unsigned sterm = 2u * (unsigned)((KS == 3 ? (ky * p.w + kx) * cs : 0) + (use1 ? cbase - p.c0 : cbase));
+        const f16* sb = use1 ? p.src1 : p.src0;
+        const unsigned bias = 2u * (unsigned)(pshift * cs);
+        const unsigned sbytes = use1 ? bytes1 : bytes0;
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)sb + sterm - bias, sbytes + bias - sterm);
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.wt + 2 * k0, wbytes - 2 * k0);
+        const int lim = p.cin - cbase;                              // only binds on a channel tail
         char* base = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < AI; ++i) {
-            const bool v = ((a_mask[i] >> tap) & 1u) && (cbase + a_ch[i] < p.cin);
-            const int off = (use1 ? a_off1[i] : a_off0[i]) + sterm;
-            const f16* src = v ? sb + off : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + (wave * AI + i) * 1024), 16, 0, 0);
+            bool v = (a_mask[i] >> tap) & 1u;
+            if (ctail) v = v && a_ch[i] < lim;
+            const unsigned off = v ? (use1 ? a_off1[i] : a_off0[i]) : kOOB;
+            dma_piece(ra, base + (wave * AI + i) * 1024, off);
         }
 #pragma unroll
-        for (int i = 0; i < BI; ++i) {
-            const f16* src = b_src[i] ? b_src[i] + k0 : zero;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(base + A_BYTES + (wave * BI + i) * 1024), 16, 0, 0);
-        }
+        for (int i = 0; i < BI; ++i)
+            dma_piece(rb, base + A_BYTES + (wave * BI + i) * 1024, b_off[i]);
+        cbase += 64;                                               // issues come in K order
+        if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
     };
 
-    // ---- fragment read offsets (loop invariant)
-    int fa_off[2][WT], fb_off[2][WT];
+    // ---- fragment read offsets: tile t of this wave = base + t * 2 KiB (the swizzle
+    // depends only on row bits 1..3, i.e. on the lane)
+    int fa0[2], fb0[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-        const int ch = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int t = 0; t < WT; ++t) {
-            fa_off[kk][t] = lds_off(wm * WT * 16 + t * 16 + (lane & 15), ch);
-            fb_off[kk][t] = A_BYTES + lds_off(wn * WT * 16 + t * 16 + (lane & 15), ch);
-        }
+        const int l = lds_off(lane & 15, kk * 4 + (lane >> 4));
+        fa0[kk] = wm * TM * 2048 + l;
+        fb0[kk] = A_BYTES + wn * TN * 2048 + l;
     }
 
-    f32x4 acc[WT][WT];
+    f32x4 acc[TN][TM];
 #pragma unroll
-    for (int a = 0; a < WT; ++a)
+    for (int a = 0; a < TN; ++a)
 #pragma unroll
-        for (int b = 0; b < WT; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
     const int nk = p.kpad / 64;
 #pragma unroll
@@ -493,30 +529,32 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         const char* S = smem + rd * STAGE;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            f16x8 fa[WT], fb[WT];
+            f16x8 fa[TM], fb[TN];
 #pragma unroll
-            for (int t = 0; t < WT; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + fa_off[kk][t]);
+            for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + fb0[kk] + t * 2048);
 #pragma unroll
-            for (int t = 0; t < WT; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + fb_off[kk][t]);
+            for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + fa0[kk] + t * 2048);
+            __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int a = 0; a < WT; ++a)
+            for (int b = 0; b < TM; ++b)
 #pragma unroll
-                for (int b = 0; b < WT; ++b)
+                for (int a = 0; a < TN; ++a)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
         }
         rd = (rd + 1 == STAGES) ? 0 : rd + 1;
         wr = (wr + 1 == STAGES) ? 0 : wr + 1;
     }
-    epilogue_tiles<WT, WT>(p, acc, m0 + wm * WT * 16, n0 + wn * WT * 16, lane);
+    epilogue_chunked<TM, TN>(p, acc, m0 + wm * TM * 16, n0 + wn * TN * 16, lane);
 }
 
-template <int WM, int WN, int WT, int STAGES, int KS>
+template <int WM, int WN, int TM, int TN, int STAGES, int KS>
 static void launch_dma(const IgemmParams& p, hipStream_t s) {
-    constexpr int smem = STAGES * (WM + WN) * WT * 16 * 128;
-    auto k = igemm_dma_kernel<WM, WN, WT, STAGES, KS>;
+    constexpr int smem = STAGES * (WM * TM + WN * TN) * 16 * 128;
+    auto k = igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>;
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
         attr = true;
     }
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy), dim3(64 * WM * WN), smem, s, p);
@@ -539,6 +577,58 @@ static int gemm_mode() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_GEMM_MODE"); v = e ? atoi(e) : 0; }
     return v;
+}
+
+// C2D_GEMM_TILE=k forces DMA tile config k (shape sweeps); 0 = heuristic.
+static int gemm_tile() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GEMM_TILE"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
+template <int WM, int WN, int TM, int TN, int ST>
+static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    p.gx = (cout + BN - 1) / BN;
+    p.gy = (p.M + BM - 1) / BM;
+    if (ksize == 1) launch_dma<WM, WN, TM, TN, ST, 1>(p, s);
+    else launch_dma<WM, WN, TM, TN, ST, 3>(p, s);
+}
+
+// Tile choice: estimated time = rounds of resident blocks x block work / per-CU
+// rate, rates measured on gfx950 for these kernels (TFLOP/s per CU with the CU
+// full); the 128x320 tile fits SD's channel counts (all multiples of 320) with no
+// column waste but has an odd per-wave column-tile count, so GEGLU skips it.
+struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
+static const DmaTile kDmaTiles[] = {
+    {7, 128, 320, 1, 3.1f, false},
+    {1, 256, 128, 1, 2.9f, true},
+    {2, 128, 128, 1, 2.2f, true},
+    {3, 64, 64, 3, 1.9f, true},
+};
+
+static int pick_dma_tile(long M, int cout, bool geglu) {
+    int best = 3;
+    double best_t = 1e300;
+    for (const DmaTile& t : kDmaTiles) {
+        if (geglu && !t.geglu) continue;
+        const long blocks = ((M + t.bm - 1) / t.bm) * ((cout + t.bn - 1) / t.bn);
+        const long slots = 256L * t.occ;
+        const double est = (double)((blocks + slots - 1) / slots) * t.bm * t.bn * t.occ / t.rate;
+        if (est < best_t) { best_t = est; best = t.id; }
+    }
+    return best;
+}
+
+static void dispatch_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
+    int id = gemm_tile();
+    if (id == 0 || (id == 7 && p.act == C2D_ACT_GEGLU)) id = pick_dma_tile(p.M, cout, p.act == C2D_ACT_GEGLU);
+    switch (id) {
+        case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
+        case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64
+        case 2: return run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s);   // 128x128, 4 waves of 64x64
+        default: return run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s);  // 64x64, 4 waves of 32x32
+    }
 }
 
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
@@ -589,21 +679,13 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
     const int mode = gemm_mode();  // 0 auto, 2 register-staged only
+    const size_t src_bytes = (size_t)d->n * d->h * d->w * (size_t)(d->c0 > d->c1 ? d->c0 : d->c1) * 2;
     const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && mode != 2 &&
-                     (d->c1 == 0 || (d->c0 & 63) == 0);
-    const long t256 = (long)((p.M + 255) / 256) * ((d->cout + 127) / 128);
+                     (d->c1 == 0 || (d->c0 & 63) == 0) && src_bytes < (1u << 31) &&
+                     (size_t)d->cout * d->kpad * 2 < (1u << 31);  // 32-bit buffer offsets
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        if (d->cout >= 128 && t256 >= 384) {
-            p.gx = (d->cout + 127) / 128; p.gy = (p.M + 255) / 256;
-            if (d->ksize == 1) launch_dma<4, 2, 4, 3, 1>(p, s); else launch_dma<4, 2, 4, 3, 3>(p, s);
-        } else if (d->cout >= 128 && t128 >= 256) {
-            p.gx = (d->cout + 127) / 128; p.gy = (p.M + 127) / 128;
-            if (d->ksize == 1) launch_dma<2, 2, 4, 3, 1>(p, s); else launch_dma<2, 2, 4, 3, 3>(p, s);
-        } else {
-            p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
-            if (d->ksize == 1) launch_dma<2, 2, 2, 3, 1>(p, s); else launch_dma<2, 2, 2, 3, 3>(p, s);
-        }
+        dispatch_dma(p, d->ksize, d->cout, s);
     } else if (t128 < 512) {
         p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
         if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);

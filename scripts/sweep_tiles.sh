@@ -1,0 +1,6 @@
+#!/bin/bash
+# Per-shape GEMM timings for each forced DMA tile config (C2D_GEMM_TILE), one process each.
+for t in ${TILES:-0 1 2 3 7}; do
+  echo "== tile $t"
+  C2D_GEMM_TILE=$t timeout -k 10 120 python scripts/bench_gemm.py || exit 1
+done
