@@ -13,7 +13,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must be loaded first: the library binds to torch's libamdhip64.so.7)
 
-LIB_PATH = Path(__file__).resolve().parent / "libc2d_hip.so"
+LIB_PATH = Path(os.environ.get("C2D_LIB") or Path(__file__).resolve().parent / "libc2d_hip.so")  # C2D_LIB: A/B builds
 
 C2D_PRO_NONE, C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_SILU = 0, 1, 2, 3
 C2D_ACT = {None: 0, "none": 0, "geglu": 1, "gelu": 2, "relu": 3, "silu": 4}

@@ -23,10 +23,14 @@ ARCH = "gfx950"
 SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I", str(ROOT / "include")]
+# attention rescales its MFMA accumulators with VALU every tile: keep them in
+# arch VGPRs (gfx950 MFMA can write them) instead of AGPRs + accvgpr copies
+EXTRA = {"attention.hip": ["-Xarch_device", "-mllvm=-amdgpu-mfma-vgpr-form=true"]}
 
 
 def _digest() -> str:
     h = hashlib.sha256()
+    h.update(repr((FLAGS, EXTRA)).encode())
     for f in sorted(CSRC.iterdir()):
         if f.suffix in (".hip", ".h", ".cpp"):
             h.update(f.name.encode())
@@ -38,7 +42,7 @@ def _digest() -> str:
 
 def _compile(src: str, build_dir: Path) -> Path:
     obj = build_dir / (Path(src).stem + ".o")
-    cmd = [HIPCC, *FLAGS, "-c", str(CSRC / src), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *EXTRA.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")

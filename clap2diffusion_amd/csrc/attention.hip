@@ -26,9 +26,10 @@ template <int D> struct AttnCfg {
     static constexpr int NLD = (64 * DCH + 255) / 256; // staged chunks per thread per tile
     static constexpr int K_BYTES = 64 * KS;
     static constexpr int V_BYTES = 64 * VS;
+    static constexpr bool SUM_MFMA = DV > D;           // a spare V column carries the row sum
 };
 
-template <int D>
+template <int D, bool MASK>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
@@ -51,9 +52,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
         int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
         *reinterpret_cast<f16x8*>(Ks + row * C::KS + ch * 16) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
     }
+    // V pad columns: zeros, except column D = 1.0 when there is one, so the PV
+    // product also accumulates the softmax row sum (SUM_MFMA)
     for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 256) {
         int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
-        *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        f16x8 z = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        if (ch == C::DCH) z[0] = (f16)1.0f;
+        *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = z;
     }
 
     // Q fragments (B operand of S^T = K Q^T): query q0 + 16 qg + li, d = 32 dc + 8 g .. +7
@@ -86,13 +91,12 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
         for (int i = 0; i < C::NLD; ++i) {
             const int idx = tid + 256 * i;
             const int row = idx / C::DCH, ch = idx - row * C::DCH;
-            const int key = t * 64 + row;
-            if (idx < 64 * C::DCH && key < lk) {
+            // keys past lk re-read the last key: their scores are masked to -inf,
+            // so their V rows meet P = 0
+            const int key = min(t * 64 + row, lk - 1);
+            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
                 rk[i] = *reinterpret_cast<const f16x8*>(kbase + (size_t)key * ldk + ch * 8);
                 rv[i] = *reinterpret_cast<const f16x8*>(vbase + (size_t)key * ldv + ch * 8);
-            } else {
-                rk[i] = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
-                rv[i] = rk[i];
             }
         }
     };
@@ -100,7 +104,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
 #pragma unroll
         for (int i = 0; i < C::NLD; ++i) {
             const int idx = tid + 256 * i;
-            if (idx < 64 * C::DCH) {
+            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
                 const int row = idx / C::DCH, ch = idx - row * C::DCH;
                 *reinterpret_cast<f16x8*>(Ks + row * C::KS + ch * 16) = rk[i];
                 *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = rv[i];
@@ -133,7 +137,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
                     s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], s[qg][kg], 0, 0, 0);
             }
         }
-        if ((t + 1) * 64 > lk) {  // tail tile: mask keys >= lk
+        if (MASK && (t + 1) * 64 > lk) {  // tail tile: mask keys >= lk
 #pragma unroll
             for (int kg = 0; kg < 4; ++kg)
 #pragma unroll
@@ -154,21 +158,27 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
                 for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qg][kg][r]);
             mx = fmaxf(mx, __shfl_xor(mx, 16));
             mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float m_new = fmaxf(m_run[qg], mx * scale_log2);
-            const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_new);
-            m_run[qg] = m_new;
+            // lazy rescale: the running max only moves (and O, l get rescaled) when
+            // some query of the wave gains more than 2^8; otherwise P <= 256 in fp16
+            const float m_cand = fmaxf(m_run[qg], mx * scale_log2);
+            if (__builtin_amdgcn_ballot_w64(m_cand > m_run[qg] + 8.0f)) {
+                const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_cand);
+                m_run[qg] = m_cand;
+                if (!C::SUM_MFMA) l_run[qg] *= alpha;
+#pragma unroll
+                for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
+            }
+            const float m_use = m_run[qg];
             float rs = 0.f;
 #pragma unroll
             for (int kg = 0; kg < 4; ++kg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], scale_log2, -m_new));
+                    const float pv = __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], scale_log2, -m_use));
                     s[qg][kg][r] = pv;
-                    rs += pv;
+                    if (!C::SUM_MFMA) rs += pv;
                 }
-            l_run[qg] = l_run[qg] * alpha + rs;
-#pragma unroll
-            for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
+            if (!C::SUM_MFMA) l_run[qg] += rs;
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -210,9 +220,15 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
     // ---- epilogue: lane holds O[query li][d = 16 dt + 4 g + r]
 #pragma unroll
     for (int qg = 0; qg < 2; ++qg) {
-        float l = l_run[qg];
-        l += __shfl_xor(l, 16);
-        l += __shfl_xor(l, 32);
+        float l;
+        if (C::SUM_MFMA) {
+            // row sum sits in O^T column D: d-tile D/16, lane group (D%16)/4, element D%4
+            l = __shfl(acc[D / 16][qg][D % 4], li + 16 * ((D % 16) / 4));
+        } else {
+            l = l_run[qg];
+            l += __shfl_xor(l, 16);
+            l += __shfl_xor(l, 32);
+        }
         const float inv = 1.0f / l;
         const int qi = q0 + qg * 16 + li;
         if (qi >= lq) continue;
@@ -237,8 +253,12 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
     const int nqb = (lq + 127) / 128;
     const int smem = C::K_BYTES + C::V_BYTES;
     dim3 grid(nqb * batch * heads);
-    hipLaunchKernelGGL((attn_fwd_kernel<D>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
-                       (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
+    if (lk % 64 == 0)
+        hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
+                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
+    else
+        hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
+                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
     return check_launch();
 }
 
