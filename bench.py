@@ -64,8 +64,50 @@ def measure_dominant_kernel(dev, iters: int = 20):
     tflops = flop / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
-            "kernel": "igemm_dma_kernel<4,2,4,3,3> (256x128 tile) conv 320->320 @ N16x64x64",
+            "kernel": "igemm_dma_kernel (c2d_conv2d_igemm) level-0 ResnetBlock2D conv 3x3 320->320 + residual, "
+                      "N=16 (CFG pair x 8 images) x 64x64",
             "flop_per_launch": flop, "avg_us": round(ms * 1e3, 2)}
+
+
+def pmc_traffic(timeout_s: int = 120):
+    """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters, one
+    counter per pass (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE (KiB, reported
+    at half the bytes of wide streaming reads on gfx950, so doubled) + WRITE_SIZE
+    (KiB, exact for 16-B/lane stores).  The passes run scripts/roof_kernel.py (the
+    same launch as measure_dominant_kernel) in a child process; None if rocprofv3
+    is unavailable or a pass fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    with tempfile.TemporaryDirectory() as td:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(td, ctr)
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+                   sys.executable, str(ROOT / "scripts" / "roof_kernel.py"), "4"]
+            try:
+                subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s,
+                               check=True)
+            except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench
+                return None, f"{ctr} pass failed: {type(e).__name__}"
+            got = []
+            for root, _, files in os.walk(d):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        for r in csv.DictReader(open(os.path.join(root, f))):
+                            if "igemm" in r["Kernel_Name"] and r["Counter_Name"] == ctr:
+                                got.append(float(r["Counter_Value"]))
+            if not got:
+                return None, f"{ctr}: no igemm rows"
+            got.sort()
+            vals[ctr] = got[len(got) // 2]
+    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    return traffic, f"rocprofv3 --pmc: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB (x2, gfx950) + WRITE_SIZE " \
+                    f"{vals['WRITE_SIZE']:.0f} KiB per launch"
 
 
 def cpu_baseline(calls: int = 2):
@@ -100,6 +142,7 @@ def main():
     ap.add_argument("--ddim-steps", type=int, default=50)
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -162,7 +205,13 @@ def main():
         roof = measure_dominant_kernel(dev)
         unet_tf = UNET_GFLOP_PER_SAMPLE * (a.res / 512) ** 2 * 2 * a.ddim_steps * world * B * a.steps / dt / 1e3
         roof["pipeline_unet_tflops"] = round(unet_tf, 2)
-        cpu = None if a.no_cpu_baseline else cpu_baseline()
+        n_, h_, c_ = 16, 64, 320
+        roof["algorithmic_bytes"] = 2 * (3 * n_ * h_ * h_ * c_ + c_ * 9 * c_)  # x + resid + out + weights
+        if not a.no_pmc and world == 1:
+            tr, src = pmc_traffic()
+            roof["traffic"] = None if tr is None else round(tr)
+            roof["traffic_source"] = src
+        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline()
         line = {
             "metric": "512x512 images/sec @ 50 DDIM steps, batch=8, 1/2/4/8 MI355X",
             "value": round(value, 4), "unit": "images/sec", "n_gpus": world, "steps": a.steps,

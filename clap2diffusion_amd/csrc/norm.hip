@@ -96,46 +96,62 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
     }
 }
 
+// grid (n, group chunks): a block owns gpb = 256 / cpg whole groups of one image.
+// Thread t sums channel (c_begin + t)'s per-block moments over the nblk partial
+// blocks (coalesced float2 loads, fixed order, fp64); each group then folds its
+// cpg channel totals in fixed order -> mean / rstd -> the per-(image, channel)
+// affine tables.
 __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
                                                           int c0, int c1, int hw, int groups, int nblk, float eps,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           const float* __restrict__ ws, float* __restrict__ scale,
                                                           float* __restrict__ shift) {
-    __shared__ float g_mean[128], g_rstd[128];
+    __shared__ double csum[256], csq[256];
+    __shared__ float g_mean[256], g_rstd[256];
     const int cin = c0 + c1, cpg = cin / groups;
-    const int n = blockIdx.x;
+    const int gpb = 256 / cpg;
+    const int n = blockIdx.x, g0 = blockIdx.y * gpb;
+    const int ng = min(gpb, groups - g0);
+    const int c_begin = g0 * cpg, nc = ng * cpg;
+    const int t = threadIdx.x;
     const size_t img = (size_t)n * hw;
-    const int lpg = 256 / groups;               // lanes per group (power of two, <= 64)
-    const int g = threadIdx.x / lpg, sub = threadIdx.x - g * lpg;
-    double a = 0.0, b = 0.0;
-    if (g < groups) {
-        const int items = nblk * cpg;
-        for (int it = sub; it < items; it += lpg) {
-            const int blk = it / cpg, c = g * cpg + (it - blk * cpg);
-            const float* p = ws + (((size_t)n * nblk + blk) * cin + c) * 2;
-            a += p[0];
-            b += p[1];
+    const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * cin + c_begin + t;
+    if (t < nc) {
+        double a = 0.0, b = 0.0;
+        int blk = 0;
+        for (; blk + 4 <= nblk; blk += 4) {
+            const float2 v0 = wp[(size_t)(blk + 0) * cin], v1 = wp[(size_t)(blk + 1) * cin];
+            const float2 v2 = wp[(size_t)(blk + 2) * cin], v3 = wp[(size_t)(blk + 3) * cin];
+            a += (double)v0.x; b += (double)v0.y;
+            a += (double)v1.x; b += (double)v1.y;
+            a += (double)v2.x; b += (double)v2.y;
+            a += (double)v3.x; b += (double)v3.y;
         }
+        for (; blk < nblk; ++blk) {
+            const float2 v = wp[(size_t)blk * cin];
+            a += (double)v.x; b += (double)v.y;
+        }
+        csum[t] = a;
+        csq[t] = b;
     }
-    for (int o = lpg >> 1; o > 0; o >>= 1) {
-        a += __shfl_xor(a, o);
-        b += __shfl_xor(b, o);
-    }
-    if (g < groups && sub == 0) {
+    __syncthreads();
+    if (t < ng) {
+        double a = 0.0, b = 0.0;
+        for (int i = 0; i < cpg; ++i) { a += csum[t * cpg + i]; b += csq[t * cpg + i]; }
         const double cnt = (double)hw * cpg;
         const double m1 = a / cnt;
         double var = b / cnt - m1 * m1;
         if (var < 0.0) var = 0.0;
-        const float s = gn_read(s0, s1, c0, c1, img, g * cpg);
-        g_mean[g] = (float)(s + m1);
-        g_rstd[g] = (float)(1.0 / sqrt(var + (double)eps));
+        const float sft = gn_read(s0, s1, c0, c1, img, (g0 + t) * cpg);
+        g_mean[t] = (float)(sft + m1);
+        g_rstd[t] = (float)(1.0 / sqrt(var + (double)eps));
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < cin; c += blockDim.x) {
-        const int gg = c / cpg;
-        const float sc = gamma[c] * g_rstd[gg];
+    if (t < nc) {
+        const int c = c_begin + t, gl = t / cpg;
+        const float sc = gamma[c] * g_rstd[gl];
         scale[(size_t)n * cin + c] = sc;
-        shift[(size_t)n * cin + c] = beta[c] - g_mean[gg] * sc;
+        shift[(size_t)n * cin + c] = beta[c] - g_mean[gl] * sc;
     }
 }
 
@@ -243,12 +259,25 @@ static int ln_dispatch(const void* x, int m, int c, int ld, float eps, float* st
 
 using namespace c2d;
 
-static const int GN_ROWS_PER_BLOCK = 128;
+// rows (pixels) per partial block: about 1024 blocks over the whole launch, at
+// least one full pass of the block's row-threads, at most 128
+static int gn_rows_per_block(int n, int c, int hw) {
+    const int nch = c >> 3;
+    const int r = nch <= 256 ? 256 / nch : 1;
+    long want = ((long)n * hw + 1023) / 1024;
+    if (want < r) want = r;
+    if (want > 128) want = 128;
+    return (int)((want + r - 1) / r * r);
+}
 
-static int gn_blocks(int hw) { return (hw + GN_ROWS_PER_BLOCK - 1) / GN_ROWS_PER_BLOCK; }
+static int gn_blocks(int n, int c, int hw) {
+    const int rpb = gn_rows_per_block(n, c, hw);
+    return (hw + rpb - 1) / rpb;
+}
 
 extern "C" size_t c2d_groupnorm_workspace_size(int n, int c, int hw) {
-    return (size_t)n * gn_blocks(hw) * c * 2 * sizeof(float);
+    if (n <= 0 || c <= 0 || hw <= 0) return 0;
+    return (size_t)n * gn_blocks(n, c, hw) * c * 2 * sizeof(float);
 }
 
 extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups,
@@ -257,14 +286,14 @@ extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, i
     if (!src0 || !gamma || !beta || !scale || !shift || !ws) return C2D_E_ARG;
     if (c1 > 0 && !src1) return C2D_E_ARG;
     const int cin = c0 + c1;
-    if ((c0 & 7) || (c1 & 7) || cin <= 0 || groups <= 0 || groups > 128 || cin % groups) return C2D_E_SHAPE;
-    if (cin > 4096 || n <= 0 || hw <= 0 || (256 % groups) || 256 / groups > 64) return C2D_E_SHAPE;
+    if ((c0 & 7) || (c1 & 7) || cin <= 0 || groups <= 0 || cin % groups) return C2D_E_SHAPE;
+    if (cin / groups > 256 || n <= 0 || hw <= 0) return C2D_E_SHAPE;
     if (!aligned16(src0) || (src1 && !aligned16(src1))) return C2D_E_ALIGN;
     hipStream_t s = (hipStream_t)stream;
     const int nch = cin >> 3;
     const int cpg = cin / groups;
-    const int rows_per_block = GN_ROWS_PER_BLOCK;
-    const int nblk = gn_blocks(hw);
+    const int rows_per_block = gn_rows_per_block(n, cin, hw);
+    const int nblk = gn_blocks(n, cin, hw);
     dim3 grid(nblk, n);
     if (nch <= 256) {
         const int R = 256 / nch;
@@ -275,7 +304,8 @@ extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, i
         hipLaunchKernelGGL((gn_partial_kernel<2>), grid, dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1,
                            hw, cpg, rows_per_block, (float*)ws);
     }
-    hipLaunchKernelGGL(gn_finalize_kernel, dim3(n), dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1, hw,
+    const int gpb = 256 / cpg;
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(n, (groups + gpb - 1) / gpb), dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1, hw,
                        groups, nblk, eps, gamma, beta, (const float*)ws, scale, shift);
     return check_launch();
 }

@@ -55,16 +55,27 @@ class AttnProcessor(nn.Module):
                 qkv[:, :inner].mul_(scale)
             o = ops.attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], b, heads, l, l, d)
         else:
-            ehs = _as_tokens(encoder_hidden_states)
-            lk = ehs.shape[1]
+            cache = cross_attention_kwargs.get("context_kv")
+            kv = cache.get(attn) if cache is not None else None
+            if kv is None:
+                kv = AttnProcessor.context_kv(self, attn, encoder_hidden_states)
+            lk = kv.shape[0] // b
             q = ops.conv(x2, attn.to_q.weight, attn.kpad_q, inner, ksize=1)
             if scale != 1.0:
                 q.mul_(scale)
-            kv = ops.conv(ehs.reshape(-1, ehs.shape[-1]), attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1)
             o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d)
         out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
                              out=None if _residual is None else _residual.reshape(b * l, c))
         return out.view(b, l, c)
+
+
+    def context_kv(self, attn, encoder_hidden_states: torch.Tensor, audio: Optional[dict] = None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """K|V = context @ [W_k; W_v]^T, [B*Lk, 2*inner] fp16 (loop-invariant across denoise steps)."""
+        ehs = _as_tokens(encoder_hidden_states.to(torch.float16))
+        inner = attn.heads * attn.dim_head
+        kv = ops.conv(ehs.reshape(-1, ehs.shape[-1]), attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1, out=out)
+        return kv
 
 
 class AudioAttnProcessor(nn.Module):
@@ -113,20 +124,18 @@ class AudioAttnProcessor(nn.Module):
         a = ops.conv(a, pk["w2"], pk["k2"], pk["n2"], ksize=1, bias=pk["b2"])
         return a.view(b, k, pk["n2"])
 
-    def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
-                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
-        if attention_mask is not None:
-            raise NotImplementedError("attention_mask is not used by the SD1.5 sampling path")
-        x = _as_tokens(hidden_states)
-        b, l, c = x.shape
-        heads, d = attn.heads, attn.dim_head
-        inner = heads * d
-        ehs = encoder_hidden_states
-        audio = cross_attention_kwargs.get("audio", None)
+    def context_kv(self, attn, encoder_hidden_states: torch.Tensor, audio: Optional[dict] = None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """K|V of the audio-injected context (reference :76-111 and :121-122), [B*Lk, 2*inner] fp16.
+
+        Depends only on the context tokens, the audio tokens and the weights, never on
+        the latent: the sampler computes it once per request (into `out`, so a
+        captured graph keeps reading the same buffer) and hands it back through
+        cross_attention_kwargs['context_kv'] on every denoise step."""
+        ehs = _as_tokens(encoder_hidden_states.to(torch.float16))
+        b = ehs.shape[0]
+        inner = attn.heads * attn.dim_head
         audio_tokens = audio[self.level] if (audio is not None and self.level in audio) else None
-        if ehs is None:  # self-attention use of the processor (reference :117-118)
-            return AttnProcessor.__call__(self, attn, hidden_states, None, None, temb, scale, _residual)
-        ehs = _as_tokens(ehs.to(torch.float16))
         kv_bias = None
         if audio_tokens is not None:
             if audio_tokens.shape[0] != b:
@@ -143,11 +152,31 @@ class AudioAttnProcessor(nn.Module):
                     proj = F.adaptive_avg_pool1d(proj.float().transpose(1, 2), 4).transpose(1, 2).to(torch.float16)
                 ehs = torch.cat([ehs, proj.to(ehs.dtype)], dim=1).contiguous()
         lk = ehs.shape[1]
+        ehs4 = ehs.view(b, 1, lk, ehs.shape[-1])
+        if out is not None:
+            out = out.view(b, 1, lk, 2 * inner)
+        kv = ops.conv(ehs4, attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1, temb=kv_bias, out=out)
+        return kv.view(b * lk, 2 * inner)
+
+    def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
+                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
+        if attention_mask is not None:
+            raise NotImplementedError("attention_mask is not used by the SD1.5 sampling path")
+        x = _as_tokens(hidden_states)
+        b, l, c = x.shape
+        heads, d = attn.heads, attn.dim_head
+        inner = heads * d
+        ehs = encoder_hidden_states
+        if ehs is None:  # self-attention use of the processor (reference :117-118)
+            return AttnProcessor.__call__(self, attn, hidden_states, None, None, temb, scale, _residual)
+        cache = cross_attention_kwargs.get("context_kv")
+        kv = cache.get(attn) if cache is not None else None
+        if kv is None:
+            kv = self.context_kv(attn, ehs, cross_attention_kwargs.get("audio", None))
+        lk = kv.shape[0] // b
         q = ops.conv(x.view(b * l, c), attn.to_q.weight, attn.kpad_q, inner, ksize=1)
         if scale != 1.0:
             q.mul_(scale)
-        ehs4 = ehs.view(b, 1, lk, ehs.shape[-1])
-        kv = ops.conv(ehs4, attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1, temb=kv_bias).view(b * lk, 2 * inner)
         o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d)
         out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
                              out=None if _residual is None else _residual.reshape(b * l, c))

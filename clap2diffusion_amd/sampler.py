@@ -6,6 +6,12 @@ CFG+DDIM update, which also advances a device-side step counter.  The step
 reads its timestep and DDIM coefficients through that counter, so the same
 graph is replayed for every step: no host work and no host<->device traffic
 inside the 50-step loop.
+
+The cross-attention K|V of every attn2 layer (text context + gated audio
+tokens, AudioAttnProcessor :76-122) does not depend on the latent: it is
+computed once per run into persistent buffers and passed to the processors as
+cross_attention_kwargs['context_kv'], so the captured step holds only the
+latent-dependent work.
 """
 from __future__ import annotations
 
@@ -23,7 +29,10 @@ class GraphDenoiser:
         self.b, self.h, self.w, self.g = batch, height, width, float(guidance)
         assert encoder_hidden_states.shape[0] == 2 * batch, "ehs must be [uncond; cond] for the CFG pair"
         self.ehs = encoder_hidden_states.to(torch.float16).contiguous()
-        self.kw = cross_attention_kwargs or {}
+        self.kw = dict(cross_attention_kwargs or {})
+        self.cross_attns = [m for m in unet.modules()
+                            if getattr(m, "is_cross_attention", False) and hasattr(m.processor, "context_kv")]
+        self.context_kv = {}
         self.t_table, self.coef = scheduler.device_tables(dev)
         self.steps = self.t_table.numel()
         self.x = torch.zeros(batch, 4, height, width, dtype=torch.float32, device=dev)
@@ -32,10 +41,17 @@ class GraphDenoiser:
         self.graph = None
         self.temb_ch = unet.cfg["block_out_channels"][0]
 
+    def prepare_context(self) -> None:
+        """(Re)compute every cross-attention K|V into its persistent buffer (eager)."""
+        audio = self.kw.get("audio")
+        for attn in self.cross_attns:
+            buf = self.context_kv.get(attn)
+            self.context_kv[attn] = attn.processor.context_kv(attn, self.ehs, audio, out=buf)
+
     def _body(self) -> None:
         xin = ops.latent_to_nhwc(self.x, self.unet.in_pad, dup=True)
         t_sin = ops.timestep_embedding(self.t_table, self.step_idx, 2 * self.b, self.temb_ch)
-        eps = self.unet.forward_nhwc(xin, t_sin, self.ehs, self.kw)
+        eps = self.unet.forward_nhwc(xin, t_sin, self.ehs, dict(self.kw, context_kv=self.context_kv))
         ops.cfg_ddim_step(eps, self.x, self.g, self.coef, self.step_idx, advance=True)
 
     def capture(self) -> None:
@@ -52,6 +68,7 @@ class GraphDenoiser:
     @torch.no_grad()
     def run(self, latents: torch.Tensor) -> torch.Tensor:
         """latents [B,4,h,w] (scaled by init_noise_sigma = 1) -> denoised latents fp32."""
+        self.prepare_context()
         if self.use_graph and self.graph is None:
             self.capture()
         self.x.copy_(latents)

@@ -101,6 +101,7 @@ int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
  * groups may straddle the seam).  ws: fp32 workspace of
  * c2d_groupnorm_workspace_size(n, c, hw) bytes holding per-block partial moments
  * (plain stores, fixed-order reduction: deterministic, no atomics, no memset).
+ * Limits: (c0 + c1) / groups <= 256 channels per group, channels multiples of 8.
  * Replaces torch.nn.GroupNorm in ResnetBlock2D.norm1/norm2 (eps 1e-5) and
  * Transformer2DModel.norm (eps 1e-6), diffusers 0.23.1.
  */

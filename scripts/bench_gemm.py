@@ -22,6 +22,12 @@ SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)
     ("L0 proj 320->320", 1, 64, 320, 320),
     ("L1 geglu 640->5120", 1, 32, 640, 5120),
     ("L2 geglu 1280->10240", 1, 16, 1280, 10240),
+    ("L1 ff2 2560->640", 1, 32, 2560, 640),
+    ("L1 qkv 640->1920", 1, 32, 640, 1920),
+    ("L2 conv 2560->1280", 3, 16, 2560, 1280),
+    ("L1 up conv 1920->640", 3, 32, 1920, 640),
+    ("L3 conv 2560->1280", 3, 8, 2560, 1280),
+    ("L2 qkv 1280->3840", 1, 16, 1280, 3840),
 ]
 
 

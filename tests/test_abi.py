@@ -40,5 +40,6 @@ def test_error_codes_without_gpu():
     d = _lib.ConvDesc()
     assert L.c2d_conv2d_igemm(ctypes.byref(d), None) == -1   # null pointers -> C2D_E_ARG
     assert L.c2d_attention_fwd(None, 0, None, 0, None, 0, None, 0, 1, 1, 1, 1, 40, 1.0, 1, None) == -1
-    assert L.c2d_groupnorm_workspace_size(2, 320, 4096) == 2 * 32 * 320 * 2 * 4
+    ws = L.c2d_groupnorm_workspace_size(2, 320, 4096)   # n * nblk * c * (sum, sumsq) fp32
+    assert ws > 0 and ws % (2 * 320 * 2 * 4) == 0 and ws // (2 * 320 * 2 * 4) <= 4096
     assert L.c2d_version().startswith(b"c2d_hip gfx950")
