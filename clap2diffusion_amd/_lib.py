@@ -21,7 +21,7 @@ ERRORS = {-1: "C2D_E_ARG", -2: "C2D_E_SHAPE", -3: "C2D_E_ALIGN", -4: "C2D_E_HIP"
 
 # every symbol include/c2d.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "c2d_conv2d_igemm", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_layernorm_stats",
+    "c2d_conv2d_igemm", "c2d_conv2d_igemm_workspace_size", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_layernorm_stats",
     "c2d_layernorm", "c2d_attention_fwd", "c2d_window_attention", "c2d_htsat_mel_patches",
     "c2d_patch_merge_gather", "c2d_row_mean", "c2d_l2_normalize", "c2d_timestep_embedding",
     "c2d_cfg_ddim_step", "c2d_latent_to_nhwc", "c2d_upsample_nearest2x", "c2d_add", "c2d_last_hip_error", "c2d_version",
@@ -37,7 +37,7 @@ class ConvDesc(ctypes.Structure):
         ("pro", c_int), ("pro_silu", c_int), ("pro_a", c_void_p), ("pro_b", c_void_p),
         ("gamma", c_void_p), ("beta", c_void_p), ("bias", c_void_p), ("act", c_int),
         ("temb", c_void_p), ("temb_ld", c_int), ("resid", c_void_p), ("resid_ld", c_int),
-        ("out", c_void_p), ("out_ld", c_int),
+        ("out", c_void_p), ("out_ld", c_int), ("ws", c_void_p), ("ws_bytes", c_size_t),
     ]
 
 
@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
     vp, i, f, sz = c_void_p, c_int, c_float, c_size_t
     sig = {
         "c2d_conv2d_igemm": ([ctypes.POINTER(ConvDesc), vp], i),
+        "c2d_conv2d_igemm_workspace_size": ([ctypes.POINTER(ConvDesc)], sz),
         "c2d_groupnorm_workspace_size": ([i, i, i], sz),
         "c2d_groupnorm_stats": ([vp, vp, i, i, i, i, i, f, vp, vp, vp, vp, vp, vp], i),
         "c2d_groupnorm_apply": ([vp, vp, i, i, i, i, vp, vp, i, vp, vp], i),

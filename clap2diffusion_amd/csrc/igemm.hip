@@ -34,6 +34,9 @@ struct IgemmParams {
     f16* out; int out_ld;
     int M;       // rows = n*oh*ow
     int gx, gy;  // tiles along cout / M
+    int ksplit;  // K slices per output tile (DMA path; 1 = no split)
+    int nkt;     // K steps per slice
+    float* ws;   // split-K fp32 partials [ksplit][M][cout]
 };
 
 // byte offset of 16-byte chunk `c` (0..7) of `row` in a [rows][64] fp16 LDS tile
@@ -423,7 +426,9 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-    const int tile = xcd_remap(blockIdx.x, p.gx * p.gy);
+    // block -> (output tile, K slice); the remap keeps a tile's slices on one XCD
+    const int bid = xcd_remap(blockIdx.x, p.gx * p.gy * p.ksplit);
+    const int tile = bid / p.ksplit, slice = bid - tile * p.ksplit;
     const int mt = tile / p.gx, nt = tile - mt * p.gx;
     const int m0 = mt * BM, n0 = nt * BN;
     const int lrow = lane >> 3, slot = lane & 7;
@@ -470,7 +475,10 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     const unsigned wbytes = (unsigned)((size_t)p.cout * p.kpad * 2);
     const bool ctail = (p.cin & 63) != 0;
 
-    int tap = 0, cbase = 0;                                       // (tap, channel block) of the next issue
+    const int nk_all = p.kpad / 64;
+    const int kb = slice * p.nkt, ke = min(nk_all, kb + p.nkt);   // this block's K steps [kb, ke)
+    int tap = 0, cbase = kb * 64;                                 // (tap, channel block) of the next issue
+    if (KS == 3) { tap = cbase / p.cin; cbase -= tap * p.cin; }
     auto issue = [&](int kt, int buf) {
         const int k0 = kt * 64;
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
@@ -514,18 +522,17 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
 #pragma unroll
         for (int b = 0; b < TM; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    const int nk = p.kpad / 64;
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
-        if (s0 < nk) issue(s0, s0);
+        if (kb + s0 < ke) issue(kb + s0, s0);
     int rd = 0, wr = STAGES - 1;
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + STAGES - 2 < nk) wait_vmcnt_le(PER * (STAGES - 2));
+    for (int kt = kb; kt < ke; ++kt) {
+        if (kt + STAGES - 2 < ke) wait_vmcnt_le(PER * (STAGES - 2));
         else wait_vmcnt_le(0);
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, wr);
+        if (kt + STAGES - 1 < ke) issue(kt + STAGES - 1, wr);
         const char* S = smem + rd * STAGE;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -545,7 +552,57 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         rd = (rd + 1 == STAGES) ? 0 : rd + 1;
         wr = (wr + 1 == STAGES) ? 0 : wr + 1;
     }
+    if (p.ksplit > 1) {
+        // raw fp32 partial sums; bias / act / temb / residual go in splitk_reduce_kernel
+        const int mw0 = m0 + wm * TM * 16, nw0 = n0 + wn * TN * 16;
+        float* dst = p.ws + (size_t)slice * p.M * p.cout;
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+            const int m = mw0 + b * 16 + (lane & 15);
+#pragma unroll
+            for (int a = 0; a < TN; ++a) {
+                const int j = nw0 + a * 16 + 4 * (lane >> 4);
+                if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = acc[a][b];
+            }
+        }
+        return;
+    }
     epilogue_chunked<TM, TN>(p, acc, m0 + wm * TM * 16, n0 + wn * TN * 16, lane);
+}
+
+// split-K combine + epilogue: out[m, j..j+3] = act(sum_s ws[s][m][j..] + bias) + temb + resid
+// (same operation order as epilogue_tiles; slices summed in fixed order)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
+    const int cq = p.cout >> 2;
+    const size_t total = (size_t)p.M * cq;
+    const int hw = p.oh * p.ow;
+    const size_t slab = (size_t)p.M * p.cout;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int m = (int)(i / cq);
+        const int j = (int)(i - (size_t)m * cq) * 4;
+        const float* src = p.ws + (size_t)m * p.cout + j;
+        f32x4 acc = *reinterpret_cast<const f32x4*>(src);
+        for (int sl = 1; sl < p.ksplit; ++sl) acc += *reinterpret_cast<const f32x4*>(src + sl * slab);
+        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+        if (p.bias) {
+            const float4 bv = *reinterpret_cast<const float4*>(p.bias + j);
+            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+        }
+        f16x4 tv, rv;
+        if (p.temb) tv = *reinterpret_cast<const f16x4*>(p.temb + (size_t)(m / hw) * p.temb_ld + j);
+        if (p.resid) rv = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
+        f16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
+            else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+            else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
+            if (p.temb) v[r] += (float)tv[r];
+            if (p.resid) v[r] += (float)rv[r];
+            o[r] = (f16)v[r];
+        }
+        *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+    }
 }
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -557,7 +614,12 @@ static void launch_dma(const IgemmParams& p, hipStream_t s) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
         attr = true;
     }
-    hipLaunchKernelGGL(k, dim3(p.gx * p.gy), dim3(64 * WM * WN), smem, s, p);
+    hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
+    if (p.ksplit > 1) {
+        const size_t total = (size_t)p.M * (p.cout >> 2);
+        const size_t want = (total + 255) / 256;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
+    }
 }
 
 template <int BM, int BN, int AMODE>
@@ -595,10 +657,12 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     else launch_dma<WM, WN, TM, TN, ST, 3>(p, s);
 }
 
-// Tile choice: estimated time = rounds of resident blocks x block work / per-CU
-// rate, rates measured on gfx950 for these kernels (TFLOP/s per CU with the CU
-// full); the 128x320 tile fits SD's channel counts (all multiples of 320) with no
-// column waste but has an odd per-wave column-tile count, so GEGLU skips it.
+// Tile / split-K choice from a cost model: estimated time = rounds of resident
+// blocks x per-block time (K steps + a fill/epilogue overhead, at the per-CU
+// rate measured on gfx950 for that tile with the CU full) + the split-K combine
+// (fp32 slabs written and read once, HBM rate, one extra launch).  The 128x320
+// tile fits SD's channel counts (all multiples of 320) with no column waste but
+// has an odd per-wave column-tile count, so GEGLU skips it; GEGLU never splits.
 struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
 static const DmaTile kDmaTiles[] = {
     {7, 128, 320, 1, 3.1f, false},
@@ -606,29 +670,75 @@ static const DmaTile kDmaTiles[] = {
     {2, 128, 128, 1, 2.2f, true},
     {3, 64, 64, 3, 1.9f, true},
 };
+struct DmaPlan { int id, split, nkt; };
 
-static int pick_dma_tile(long M, int cout, bool geglu) {
-    int best = 3;
+static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int force_split) {
+    DmaPlan best = {3, 1, nk};
     double best_t = 1e300;
+    const int splits[] = {1, 2, 3, 4, 6, 8};
     for (const DmaTile& t : kDmaTiles) {
         if (geglu && !t.geglu) continue;
-        const long blocks = ((M + t.bm - 1) / t.bm) * ((cout + t.bn - 1) / t.bn);
-        const long slots = 256L * t.occ;
-        const double est = (double)((blocks + slots - 1) / slots) * t.bm * t.bn * t.occ / t.rate;
-        if (est < best_t) { best_t = est; best = t.id; }
+        if (force_id && t.id != force_id) continue;
+        const long tiles = ((M + t.bm - 1) / t.bm) * ((cout + t.bn - 1) / t.bn);
+        for (int sp : splits) {
+            if (force_split && sp != force_split) continue;
+            if (sp > 1 && (geglu || nk < 8 * sp || tiles >= 256)) continue;
+            const int nkt = (nk + sp - 1) / sp;
+            const int eff = (nk + nkt - 1) / nkt;
+            const long blocks = tiles * eff;
+            const long slots = 256L * t.occ;
+            const double blk_us = 2.0 * t.bm * t.bn * 64.0 * (nkt + 3) * t.occ / (t.rate * 1e6);
+            double est = (double)((blocks + slots - 1) / slots) * blk_us;
+            if (eff > 1) est += (double)M * cout * 4.0 * (eff + 1) / 4e6 + 2.0;
+            if (est < best_t) { best_t = est; best = {t.id, eff, nkt}; }
+        }
     }
     return best;
 }
 
-static void dispatch_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
+// C2D_GEMM_SPLIT=s forces s K slices (when the workspace allows); 0 = model
+static int gemm_split() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GEMM_SPLIT"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
+static DmaPlan plan_for(long M, int cout, int kpad, int act) {
+    const bool geglu = act == C2D_ACT_GEGLU;
     int id = gemm_tile();
-    if (id == 0 || (id == 7 && p.act == C2D_ACT_GEGLU)) id = pick_dma_tile(p.M, cout, p.act == C2D_ACT_GEGLU);
-    switch (id) {
+    if (id == 7 && geglu) id = 0;
+    DmaPlan pl = plan_dma(M, cout, kpad / 64, geglu, id, gemm_split());
+    if (pl.id == 0) pl = plan_dma(M, cout, kpad / 64, geglu, 0, 0);
+    return pl;
+}
+
+static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout, hipStream_t s) {
+    p.ksplit = pl.split;
+    p.nkt = pl.nkt;
+    switch (pl.id) {
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
         case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64
         case 2: return run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s);   // 128x128, 4 waves of 64x64
         default: return run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s);  // 64x64, 4 waves of 32x32
     }
+}
+
+// does this descriptor run on the LDS-DMA kernels (no prologue, buffer-offset limits)?
+static bool dma_eligible(const c2d_conv_desc* d) {
+    const int cin = d->c0 + d->c1;
+    const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
+    const size_t src_bytes = (size_t)d->n * d->h * d->w * (size_t)(d->c0 > d->c1 ? d->c0 : d->c1) * 2;
+    return (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && gemm_mode() != 2 &&
+           (d->c1 == 0 || (d->c0 & 63) == 0) && src_bytes < (1u << 31) &&
+           (size_t)d->cout * d->kpad * 2 < (1u << 31);  // 32-bit buffer offsets
+}
+
+extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
+    if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
+    if (!dma_eligible(d)) return 0;
+    const long M = (long)d->n * d->oh * d->ow;
+    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act);
+    return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
 
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
@@ -678,14 +788,23 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
 
     hipStream_t s = (hipStream_t)stream;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
-    const int mode = gemm_mode();  // 0 auto, 2 register-staged only
-    const size_t src_bytes = (size_t)d->n * d->h * d->w * (size_t)(d->c0 > d->c1 ? d->c0 : d->c1) * 2;
-    const bool dma = (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && mode != 2 &&
-                     (d->c1 == 0 || (d->c0 & 63) == 0) && src_bytes < (1u << 31) &&
-                     (size_t)d->cout * d->kpad * 2 < (1u << 31);  // 32-bit buffer offsets
+    const bool dma = dma_eligible(d);
+    p.ksplit = 1;
+    p.nkt = d->kpad / 64;
+    p.ws = nullptr;
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        dispatch_dma(p, d->ksize, d->cout, s);
+        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act);
+        if (pl.split > 1) {
+            const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
+            if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {
+                p.ws = (float*)d->ws;
+            } else {  // no / short workspace: same tile, one K slice
+                pl.split = 1;
+                pl.nkt = d->kpad / 64;
+            }
+        }
+        dispatch_dma(p, pl, d->ksize, d->cout, s);
     } else if (t128 < 512) {
         p.gx = (d->cout + 63) / 64; p.gy = (p.M + 63) / 64;
         if (amode == AM_1X1) launch<64, 64, AM_1X1>(p, s);

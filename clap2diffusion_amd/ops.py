@@ -113,6 +113,10 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
     d.out = ptr(out)
     d.out_ld = out.stride(-2) if out.dim() == 2 else out.shape[-1]
     assert out.stride(-1) == 1
+    wsb = lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
+    if wsb:
+        ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
+        d.ws = ptr(ws); d.ws_bytes = wsb
     check(lib().c2d_conv2d_igemm(ctypes.byref(d), stream_ptr()), "c2d_conv2d_igemm")
     return out
 

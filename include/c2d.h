@@ -89,9 +89,20 @@ typedef struct c2d_conv_desc {
     int resid_ld;
     void* out;               /* fp16 [m][out_ld]                                          */
     int out_ld;
+    void* ws;                /* optional split-K workspace (16-B aligned) or NULL         */
+    size_t ws_bytes;         /* its size; below c2d_conv2d_igemm_workspace_size(): no split */
 } c2d_conv_desc;
 
 int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
+
+/*
+ * Bytes of fp32 split-K workspace c2d_conv2d_igemm would use for this descriptor
+ * (0 = the shape fills the chip without splitting K).  Under-filled GEMMs (the
+ * 16x16 / 8x8 UNet levels: 80-160 output tiles on 256 CUs) split K across blocks
+ * into [split][m][cout] fp32 slabs that a second, stream-ordered kernel sums in
+ * fixed order before the epilogue (deterministic; no atomics).
+ */
+size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d);
 
 /*
  * GroupNorm statistics folded with the affine into per-(image, channel) scale /

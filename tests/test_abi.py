@@ -40,6 +40,12 @@ def test_error_codes_without_gpu():
     d = _lib.ConvDesc()
     assert L.c2d_conv2d_igemm(ctypes.byref(d), None) == -1   # null pointers -> C2D_E_ARG
     assert L.c2d_attention_fwd(None, 0, None, 0, None, 0, None, 0, 1, 1, 1, 1, 40, 1.0, 1, None) == -1
+    d = _lib.ConvDesc()   # L3 (8x8) resnet conv at N=16: under-filled -> split-K workspace
+    d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride, d.cout, d.kpad = 1280, 16, 8, 8, 8, 8, 3, 1, 1280, 11520
+    assert L.c2d_conv2d_igemm_workspace_size(ctypes.byref(d)) % (16 * 64 * 1280 * 4) == 0
+    assert L.c2d_conv2d_igemm_workspace_size(ctypes.byref(d)) >= 2 * 16 * 64 * 1280 * 4
+    d.c0, d.h, d.w, d.oh, d.ow, d.cout, d.kpad = 320, 64, 64, 64, 64, 320, 2880   # L0: fills the chip
+    assert L.c2d_conv2d_igemm_workspace_size(ctypes.byref(d)) == 0
     ws = L.c2d_groupnorm_workspace_size(2, 320, 4096)   # n * nblk * c * (sum, sumsq) fp32
     assert ws > 0 and ws % (2 * 320 * 2 * 4) == 0 and ws // (2 * 320 * 2 * 4) <= 4096
     assert L.c2d_version().startswith(b"c2d_hip gfx950")

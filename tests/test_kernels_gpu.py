@@ -75,6 +75,40 @@ def test_conv3x3_gn_silu_temb_resid(dev):
     close(nchw(out), ref)
 
 
+@pytest.mark.parametrize("n,h,c0,c1,cout,act", [
+    (16, 8, 1280, 0, 1280, None),       # L3 resnet conv: 80 tiles -> split-K
+    (16, 8, 1280, 1280, 1280, None),    # L3 up-block conv over the skip concat (K = 23040)
+    (16, 16, 1280, 0, 1280, "silu"),    # L2 conv with an activation through the combine kernel
+])
+def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
+    """Under-filled levels split K over blocks (fp32 slabs + combine kernel that
+    applies bias -> act -> +temb -> +resid); same numerics bar as the direct path."""
+    from clap2diffusion_amd import _lib
+    import ctypes
+    d = _lib.ConvDesc()
+    d.c0, d.c1, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = c0, c1, n, h, h, h, h, 3, 1
+    d.cout, d.kpad = cout, ops.kpad_of(9 * (c0 + c1))
+    assert _lib.lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d)) > 0, "shape expected to split K"
+    cin = c0 + c1
+    x = gen(n, cin, h, h, seed=21)
+    w = gen(cout, cin, 3, 3, seed=22, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=23)
+    temb = gen(n, cout, seed=24) if act is None else None
+    resid = gen(n, cout, h, h, seed=25)
+    ref = F.conv2d(x, w, b, padding=1)
+    if act == "silu":
+        ref = F.silu(ref)
+    if temb is not None:
+        ref = ref + temb[:, :, None, None]
+    ref = ref + resid
+    xd = nhwc(x).half().to(dev)
+    x0, x1 = (xd[..., :c0].contiguous(), xd[..., c0:].contiguous()) if c1 else (xd, None)
+    wp, kp = ops.pack_conv_weight(w)
+    out = ops.conv(x0, wp.to(dev), kp, cout, ksize=3, x2=x1, bias=b.float().to(dev), act=act,
+                   temb=None if temb is None else temb.half().to(dev), resid=nhwc(resid).half().to(dev))
+    close(nchw(out), ref)
+
+
 @pytest.mark.parametrize("n,h,c0,c1,cout,k", [
     (2, 8, 1280, 640, 640, 3),      # 64x64 DMA tiles
     (16, 32, 640, 320, 320, 3),     # 128x128 DMA tiles
