@@ -64,7 +64,7 @@ def measure_dominant_kernel(dev, iters: int = 20):
     tflops = flop / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
-            "kernel": "igemm_dma_kernel (c2d_conv2d_igemm) level-0 ResnetBlock2D conv 3x3 320->320 + residual, "
+            "kernel": "c2d_conv2d_igemm (igemm_m32_kernel 256x320 tile) level-0 ResnetBlock2D conv 3x3 320->320 + residual, "
                       "N=16 (CFG pair x 8 images) x 64x64",
             "flop_per_launch": flop, "avg_us": round(ms * 1e3, 2)}
 

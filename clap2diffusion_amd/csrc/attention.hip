@@ -16,9 +16,15 @@
 namespace c2d {
 
 template <int D> struct AttnCfg {
-    static constexpr int DP = (D + 31) / 32 * 32;      // K dim of QK^T, multiple of 32
+    // K dim of QK^T: full 32-deep chunks on 16x16x32 MFMAs plus, when the rest is
+    // exactly 16 deep (d = 80), one 16x16x16 MFMA into a separate accumulator
+    // (added with VALU: no mixed-shape MFMA accumulation chain) instead of a
+    // zero-padded 32 chunk
+    static constexpr int NDC = D / 32;
+    static constexpr bool TAIL = (D % 32) == 16;
+    static constexpr int DP = TAIL ? NDC * 32 + 16 : (D + 31) / 32 * 32;
+    static constexpr int NDC_FULL = TAIL ? NDC : DP / 32;  // 32-deep chunks actually issued
     static constexpr int DV = (D + 15) / 16 * 16;      // N dim of PV, multiple of 16
-    static constexpr int NDC = DP / 32;
     static constexpr int NDT = DV / 16;
     static constexpr int KS = DP * 2 + 16;             // K row stride (bytes): odd # of 16-B slots
     static constexpr int VS = (DV == 48) ? 96 : (DV == 64 || DV == 80) ? 160 : (DV == 160) ? 352 : DV * 2 + 32;
@@ -61,18 +67,26 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
         *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = z;
     }
 
-    // Q fragments (B operand of S^T = K Q^T): query q0 + 16 qg + li, d = 32 dc + 8 g .. +7
-    f16x8 qf[2][C::NDC];
+    // Q fragments (B operand of S^T = K Q^T): query q0 + 16 qg + li, d = 32 dc + 8 g .. +7;
+    // tail (16x16x16): d = 32 NDC + 4 g .. +3
+    f16x8 qf[2][C::NDC_FULL > 0 ? C::NDC_FULL : 1];
+    f16x4 qt[2];
 #pragma unroll
     for (int qg = 0; qg < 2; ++qg) {
         const int qi = q0 + qg * 16 + li;
 #pragma unroll
-        for (int dc = 0; dc < C::NDC; ++dc) {
+        for (int dc = 0; dc < C::NDC_FULL; ++dc) {
             const int d0 = dc * 32 + g * 8;
             if (qi < lq && d0 < D)
                 qf[qg][dc] = *reinterpret_cast<const f16x8*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
             else
                 qf[qg][dc] = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        qt[qg] = (f16x4){0, 0, 0, 0};
+        if (C::TAIL) {
+            const int d0 = C::NDC * 32 + g * 4;
+            if (qi < lq && d0 < D)
+                qt[qg] = *reinterpret_cast<const f16x4*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
         }
     }
 
@@ -122,7 +136,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
         if (t + 1 < ntiles) gload(t + 1);
 
         // ---- S^T tiles: s[qg][kg] holds keys 16 kg + 4 g + r of query li
-        f32x4 s[2][4];
+        f32x4 s[2][4], st[2][4];
 #pragma unroll
         for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
@@ -130,12 +144,24 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
 #pragma unroll
         for (int kg = 0; kg < 4; ++kg) {
 #pragma unroll
-            for (int dc = 0; dc < C::NDC; ++dc) {
+            for (int dc = 0; dc < C::NDC_FULL; ++dc) {
                 const f16x8 kf = *reinterpret_cast<const f16x8*>(Ks + (kg * 16 + li) * C::KS + (dc * 4 + g) * 16);
 #pragma unroll
                 for (int qg = 0; qg < 2; ++qg)
                     s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], s[qg][kg], 0, 0, 0);
             }
+            if (C::TAIL) {
+                const f16x4 kt = *reinterpret_cast<const f16x4*>(Ks + (kg * 16 + li) * C::KS + C::NDC * 64 + g * 8);
+#pragma unroll
+                for (int qg = 0; qg < 2; ++qg)
+                    st[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x16f16(kt, qt[qg], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            }
+        }
+        if (C::TAIL) {
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+                for (int kg = 0; kg < 4; ++kg) s[qg][kg] += st[qg][kg];
         }
         if (MASK && (t + 1) * 64 > lk) {  // tail tile: mask keys >= lk
 #pragma unroll

@@ -1,0 +1,106 @@
+// Shared GEMM epilogue body for the implicit-GEMM kernels (included by igemm.hip
+// after IgemmParams).  The MFMA kernels first write their fp32 accumulators as
+// a row-major image into the (now free) LDS staging ring; epi_rows then applies
+//   out[m, j] = act(acc + bias[j]) + temb[n(m), j] + resid[m, j]
+//   (GEGLU: (h + bh) * gelu(g + bg) [+ resid], packed [16 h | 16 g] per 32 rows)
+// in one compact loop over 16-B output chunks: coalesced 16-B loads / stores,
+// one fp16 rounding at the end, and a few hundred instructions of code instead
+// of a fully unrolled per-register epilogue (which ran to ~50k instructions with
+// the runtime activation branches and thrashed the instruction cache).
+#pragma once
+
+namespace c2d {
+
+// W-column chunk body (W = 8: 16-B loads / stores; W = 4: 8-B, for outputs whose
+// width, leading dimensions or base addresses are only 4-element aligned, e.g. the
+// 4-channel conv_out).  img: fp32 [rows][pitchf] image of the block's rows m0..
+// and packed weight columns jp0 .. jp0 + cols (cols % 8 == 0; GEGLU: % 32 == 0).
+template <int W>
+__device__ __forceinline__ void epi_rows_w(const IgemmParams& p, const float* img, int pitchf, int rows, int cols,
+                                           int m0, int jp0, int lane) {
+    typedef _Float16 hv __attribute__((ext_vector_type(W)));
+    const bool geglu = p.act == C2D_ACT_GEGLU;
+    const int cpr = geglu ? cols / (2 * W) : cols / W;      // W-wide output chunks per row
+    const int cpt = 16 / W;                                 // GEGLU: chunks per 32-row tile
+    const int hw = p.oh * p.ow;
+    const int out_cols = geglu ? (p.cout >> 1) : p.cout;
+    for (int c = lane; c < rows * cpr; c += 64) {
+        const int row = c / cpr, cc = c - row * cpr;
+        const int m = m0 + row;
+        int sc, jp, j;                                       // image column, packed row, output column
+        if (geglu) {
+            const int t = cc / cpt, q = cc - t * cpt;
+            sc = t * 32 + q * W;
+            jp = jp0 + sc;
+            j = ((jp0 + t * 32) >> 1) + q * W;
+        } else {
+            sc = cc * W;
+            jp = jp0 + sc;
+            j = jp;
+        }
+        if (m >= p.M || j >= out_cols) continue;
+        const float* src = img + row * pitchf + sc;
+        float v[W];
+#pragma unroll
+        for (int r = 0; r < W; r += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(src + r);
+            v[r] = x.x; v[r + 1] = x.y; v[r + 2] = x.z; v[r + 3] = x.w;
+        }
+        if (p.bias) {
+#pragma unroll
+            for (int r = 0; r < W; r += 4) {
+                const float4 bb = *reinterpret_cast<const float4*>(p.bias + jp + r);
+                v[r] += bb.x; v[r + 1] += bb.y; v[r + 2] += bb.z; v[r + 3] += bb.w;
+            }
+        }
+        if (geglu) {
+            float g[W];
+#pragma unroll
+            for (int r = 0; r < W; r += 4) {
+                const float4 x = *reinterpret_cast<const float4*>(src + 16 + r);
+                g[r] = x.x; g[r + 1] = x.y; g[r + 2] = x.z; g[r + 3] = x.w;
+                if (p.bias) {
+                    const float4 bb = *reinterpret_cast<const float4*>(p.bias + jp + 16 + r);
+                    g[r] += bb.x; g[r + 1] += bb.y; g[r + 2] += bb.z; g[r + 3] += bb.w;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] *= gelu_f(g[r]);
+        } else if (p.act == C2D_ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] = gelu_f(v[r]);
+        } else if (p.act == C2D_ACT_RELU) {
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] = fmaxf(v[r], 0.f);
+        } else if (p.act == C2D_ACT_SILU) {
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] = silu_f(v[r]);
+        }
+        if (p.temb) {
+            const hv tt = *reinterpret_cast<const hv*>(p.temb + (size_t)(m / hw) * p.temb_ld + j);
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] += (float)tt[r];
+        }
+        if (p.resid) {
+            const hv rr = *reinterpret_cast<const hv*>(p.resid + (size_t)m * p.resid_ld + j);
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] += (float)rr[r];
+        }
+        hv o;
+#pragma unroll
+        for (int r = 0; r < W; ++r) o[r] = (f16)v[r];
+        *reinterpret_cast<hv*>(p.out + (size_t)m * p.out_ld + j) = o;
+    }
+}
+
+__device__ __forceinline__ void epi_rows(const IgemmParams& p, const float* img, int pitchf, int rows, int cols,
+                                         int m0, int jp0, int lane) {
+    const int out_cols = p.act == C2D_ACT_GEGLU ? (p.cout >> 1) : p.cout;
+    const uintptr_t al = (uintptr_t)p.out | (uintptr_t)p.resid | (uintptr_t)p.temb;
+    const bool wide = ((out_cols | p.out_ld | (p.resid ? p.resid_ld : 0) | (p.temb ? p.temb_ld : 0)) & 7) == 0 &&
+                      (al & 15) == 0;
+    if (wide) epi_rows_w<8>(p, img, pitchf, rows, cols, m0, jp0, lane);
+    else epi_rows_w<4>(p, img, pitchf, rows, cols, m0, jp0, lane);
+}
+
+}  // namespace c2d

@@ -37,7 +37,13 @@ struct IgemmParams {
     int ksplit;  // K slices per output tile (DMA path; 1 = no split)
     int nkt;     // K steps per slice
     float* ws;   // split-K fp32 partials [ksplit][M][cout]
+    int abl;     // timing ablation bits (C2D_GEMM_ABL; 0 in production)
+    int lds_epi; // 32x32 kernels: LDS-staged coalesced epilogue (C2D_GEMM_LDSEPI, default on)
 };
+
+}  // namespace c2d
+#include "epilogue.h"
+namespace c2d {
 
 // byte offset of 16-byte chunk `c` (0..7) of `row` in a [rows][64] fp16 LDS tile
 __device__ __forceinline__ int lds_off(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
@@ -477,6 +483,9 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
 
     const int nk_all = p.kpad / 64;
     const int kb = slice * p.nkt, ke = min(nk_all, kb + p.nkt);   // this block's K steps [kb, ke)
+    const char* u_src0 = uniform_ptr(p.src0);
+    const char* u_src1 = uniform_ptr(p.src1);
+    const char* u_wt = uniform_ptr(p.wt);
     int tap = 0, cbase = kb * 64;                                 // (tap, channel block) of the next issue
     if (KS == 3) { tap = cbase / p.cin; cbase -= tap * p.cin; }
     auto issue = [&](int kt, int buf) {
@@ -485,18 +494,19 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         const bool use1 = two && cbase >= p.c0;
         const int cs = use1 ? p.c1 : p.c0;
         const unsigned sterm = 2u * (unsigned)((KS == 3 ? (ky * p.w + kx) * cs : 0) + (use1 ? cbase - p.c0 : cbase));
-        const f16* sb = use1 ? p.src1 : p.src0;
+        const char* sb = use1 ? u_src1 : u_src0;
         const unsigned bias = 2u * (unsigned)(pshift * cs);
         const unsigned sbytes = use1 ? bytes1 : bytes0;
-        const __amdgpu_buffer_rsrc_t ra = make_rsrc((const char*)sb + sterm - bias, sbytes + bias - sterm);
-        const __amdgpu_buffer_rsrc_t rb = make_rsrc((const char*)p.wt + 2 * k0, wbytes - 2 * k0);
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc(sb + sterm - bias, sbytes + bias - sterm);
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc(u_wt + 2 * k0, wbytes - 2 * k0);
         const int lim = p.cin - cbase;                              // only binds on a channel tail
         char* base = smem + buf * STAGE;
 #pragma unroll
         for (int i = 0; i < AI; ++i) {
-            bool v = (a_mask[i] >> tap) & 1u;
-            if (ctail) v = v && a_ch[i] < lim;
-            const unsigned off = v ? (use1 ? a_off1[i] : a_off0[i]) : kOOB;
+            // branch-free: a dropped tap / channel tail pushes the offset past num_records
+            unsigned ok = (a_mask[i] >> tap) & 1u;
+            if (ctail) ok &= (unsigned)(a_ch[i] < lim);
+            const unsigned off = (use1 ? a_off1[i] : a_off0[i]) | ((ok - 1u) & kOOB);
             dma_piece(ra, base + (wave * AI + i) * 1024, off);
         }
 #pragma unroll
@@ -532,7 +542,9 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + STAGES - 1 < ke) issue(kt + STAGES - 1, wr);
+        // p.abl (timing ablation only, C2D_GEMM_ABL): bit 0 skips the DMA after the
+        // prologue stages, bit 1 skips the MFMAs (fragments still read and kept live)
+        if (kt + STAGES - 1 < ke && !(p.abl & 1)) issue(kt + STAGES - 1, wr);
         const char* S = smem + rd * STAGE;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -541,6 +553,13 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
             for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + fb0[kk] + t * 2048);
 #pragma unroll
             for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + fa0[kk] + t * 2048);
+            if (p.abl & 2) {
+#pragma unroll
+                for (int t = 0; t < TN; ++t) asm volatile("" :: "v"(fb[t]));
+#pragma unroll
+                for (int t = 0; t < TM; ++t) asm volatile("" :: "v"(fa[t]));
+                continue;
+            }
             __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int b = 0; b < TM; ++b)
@@ -567,7 +586,29 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         }
         return;
     }
-    epilogue_chunked<TM, TN>(p, acc, m0 + wm * TM * 16, n0 + wn * TN * 16, lane);
+    // LDS-staged epilogue (epilogue.h): accumulators -> fp32 image of up to 32 rows
+    // per wave, then one compact loop of coalesced 16-B chunks
+    __syncthreads();
+    {
+        constexpr int PITCHF = TN * 16 + 4;
+        constexpr int RB = TM < 2 ? TM : 2;                  // 16-row tiles per image
+        float* img = reinterpret_cast<float*>(smem) + wave * 16 * RB * PITCHF;
+        const int mw0 = m0 + wm * TM * 16, nw0 = n0 + wn * TN * 16;
+#pragma unroll
+        for (int b0 = 0; b0 < TM; b0 += RB) {
+#pragma unroll
+            for (int bb = 0; bb < RB; ++bb)
+#pragma unroll
+                for (int a = 0; a < TN; ++a)
+                    *reinterpret_cast<f32x4*>(img + (bb * 16 + (lane & 15)) * PITCHF + a * 16 + 4 * (lane >> 4)) =
+                        acc[a][b0 + bb];
+            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
+            __builtin_amdgcn_wave_barrier();
+            epi_rows(p, img, PITCHF, RB * 16, TN * 16, mw0 + b0 * 16, nw0, lane);
+            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
 }
 
 // split-K combine + epilogue: out[m, j..j+3] = act(sum_s ws[s][m][j..] + bias) + temb + resid
@@ -604,6 +645,10 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
         *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
     }
 }
+
+}  // namespace c2d
+#include "igemm_m32.h"
+namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
 static void launch_dma(const IgemmParams& p, hipStream_t s) {
@@ -665,6 +710,15 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 // has an odd per-wave column-tile count, so GEGLU skips it; GEGLU never splits.
 struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
 static const DmaTile kDmaTiles[] = {
+    // 32x32x16 MFMA, deep LDS-DMA ring (igemm_m32.h); rate 0 = only when forced (C2D_GEMM_TILE)
+    {20, 256, 320, 1, 0.0f, true},
+    {21, 256, 256, 1, 0.0f, true},
+    {22, 128, 320, 1, 0.0f, true},
+    {23, 256, 320, 1, 0.0f, true},
+    {24, 128, 256, 1, 0.0f, true},
+    {30, 256, 320, 1, 0.0f, true},
+    {31, 128, 320, 1, 0.0f, true},
+    {32, 256, 256, 1, 0.0f, true},
     {7, 128, 320, 1, 3.1f, false},
     {1, 256, 128, 1, 2.9f, true},
     {2, 128, 128, 1, 2.2f, true},
@@ -679,6 +733,7 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
     for (const DmaTile& t : kDmaTiles) {
         if (geglu && !t.geglu) continue;
         if (force_id && t.id != force_id) continue;
+        if (!force_id && t.rate <= 0.f) continue;
         const long tiles = ((M + t.bm - 1) / t.bm) * ((cout + t.bn - 1) / t.bn);
         for (int sp : splits) {
             if (force_split && sp != force_split) continue;
@@ -687,13 +742,26 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
             const int eff = (nk + nkt - 1) / nkt;
             const long blocks = tiles * eff;
             const long slots = 256L * t.occ;
-            const double blk_us = 2.0 * t.bm * t.bn * 64.0 * (nkt + 3) * t.occ / (t.rate * 1e6);
+            const double blk_us = 2.0 * t.bm * t.bn * 64.0 * (nkt + 3) * t.occ / ((t.rate > 0.f ? t.rate : 3.0f) * 1e6);
             double est = (double)((blocks + slots - 1) / slots) * blk_us;
             if (eff > 1) est += (double)M * cout * 4.0 * (eff + 1) / 4e6 + 2.0;
             if (est < best_t) { best_t = est; best = {t.id, eff, nkt}; }
         }
     }
     return best;
+}
+
+// C2D_GEMM_ABL: timing ablation of the DMA kernel (1 = no DMA, 2 = no MFMA); wrong results by design
+static int gemm_abl() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GEMM_ABL"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
+static int gemm_lds_epi() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GEMM_LDSEPI"); v = e ? atoi(e) : 1; }
+    return v;
 }
 
 // C2D_GEMM_SPLIT=s forces s K slices (when the workspace allows); 0 = model
@@ -703,19 +771,40 @@ static int gemm_split() {
     return v;
 }
 
+// Tile choice.  Measured on gfx950 over the UNet's conv / linear shapes
+// (scripts/bench_gemm.py, scripts/sweep_tiles.sh): the 256x320 32x32-MFMA tile
+// (id 23) is fastest whenever its tiles fill the chip by themselves (all level-0
+// GEMMs, the GEGLU projections, the 256-row-tile-rich up-block convs); otherwise
+// the 128x320 tile (id 7; GEGLU: 256x128, id 1) when its tiles fill the chip;
+// under-filled shapes (16x16 / 8x8 levels) go through the cost model with split-K.
 static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     const bool geglu = act == C2D_ACT_GEGLU;
+    const int nk = kpad / 64;
     int id = gemm_tile();
     if (id == 7 && geglu) id = 0;
-    DmaPlan pl = plan_dma(M, cout, kpad / 64, geglu, id, gemm_split());
-    if (pl.id == 0) pl = plan_dma(M, cout, kpad / 64, geglu, 0, 0);
-    return pl;
+    if (id) {
+        DmaPlan pl = plan_dma(M, cout, nk, geglu, id, gemm_split());
+        if (pl.id) return pl;
+    }
+    const long t23 = ((M + 255) / 256) * ((cout + 319) / 320);
+    if (t23 >= 256) return {23, 1, nk};
+    const long t7 = geglu ? ((M + 255) / 256) * ((cout + 127) / 128) : ((M + 127) / 128) * ((cout + 319) / 320);
+    if (t7 >= 256) return {geglu ? 1 : 7, 1, nk};
+    return plan_dma(M, cout, nk, geglu, 0, 0);
 }
 
 static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout, hipStream_t s) {
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
     switch (pl.id) {
+        case 20: return run_m32<4, 2, 2, 5, 32, 4, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160
+        case 21: return run_m32<4, 2, 2, 4, 32, 4, true>(p, ksize, cout, s);   // 256x256, 8 waves of 64x128
+        case 22: return run_m32<4, 2, 1, 5, 32, 4, true>(p, ksize, cout, s);   // 128x320, 8 waves of 32x160
+        case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, BK 64, 2 stages
+        case 24: return run_m32<2, 2, 2, 4, 32, 6, true>(p, ksize, cout, s);   // 128x256, 4 waves of 64x128
+        case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
+        case 31: return run_pp<4, 2, 1, 5>(p, ksize, cout, s);   // 128x320 ping-pong, 8 waves of 32x160
+        case 32: return run_pp<4, 2, 2, 4>(p, ksize, cout, s);   // 256x256 ping-pong, 8 waves of 64x128
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
         case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64
         case 2: return run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s);   // 128x128, 4 waves of 64x64
@@ -792,6 +881,8 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.ksplit = 1;
     p.nkt = d->kpad / 64;
     p.ws = nullptr;
+    p.abl = gemm_abl();
+    p.lds_epi = gemm_lds_epi();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
         DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act);

@@ -1,0 +1,533 @@
+// Implicit-GEMM conv / linear on v_mfma_f32_32x32x16_f16 with a deep LDS-DMA
+// ring.  Included by igemm.hip (uses IgemmParams, dma_piece, make_rsrc, kOOB,
+// splitk_reduce_kernel from there).
+//
+// Why 32x32x16: at equal wave tile it reads half the LDS bytes per MAC of the
+// 16x16x32 form (TM + TN fragments per TM*TN MFMAs of 32x32x16).  Why a deep
+// ring of short stages: the conv kernels are bound by how many bytes each CU
+// keeps in flight from L2 / MALL into LDS (PMC: MFMA busy 35 %, waves parked on
+// vmcnt / barrier 36 % with one 56-72 KiB stage in flight); BK = 32 stages let
+// three stages (~100 KiB) stay in flight behind the MFMAs in the same LDS.
+#pragma once
+
+namespace c2d {
+
+// ---------------------------------------------------------------------------
+// LDS image per stage: [BM rows | BN rows] of BK fp16 (RB = 2 BK bytes per
+// row), 16-B chunks XOR-swizzled so the 32-row fragment reads are
+// conflict-free (each ds_read_b128 lane group of 16 hits 16 distinct slots):
+//   BK 64: chunk c of row r at slot c ^ ((r >> 1) & 7)
+//   BK 32: chunk c of row r at slot c ^ ((r >> 2) & 3)
+template <int BK>
+__device__ __forceinline__ int lds_sw(int row, int c) {
+    if (BK == 64) return row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+    return row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
+}
+
+// LDS-DMA staging of one BK-deep K step of the A (im2col rows) and B (packed
+// weight rows) tiles.  Same addressing as igemm_dma_kernel: per staged row a
+// pixel index + a 3x3 tap mask, the wave-uniform (tap, channel block) part of
+// the address folded into the buffer descriptor base, halo / tail lanes pushed
+// past num_records (the buffer unit returns zeros).  A piece (one 1-KiB DMA wave
+// instruction) covers RPP = 1024 / RB rows; the NA + NB pieces of a stage are
+// dealt round-robin to the NW waves, A first (NA % NW == 0, so piece slot i is
+// an A slot for i < NA / NW in every wave; the last B slot may be partial).
+template <int BM, int BN, int BK, int NW, int KS>
+struct M32Loader {
+    static constexpr int RB = 2 * BK, RPP = 1024 / RB, CPR = BK / 8;
+    static constexpr int NA = BM / RPP, NB = BN / RPP;
+    static constexpr int SA = NA / NW;
+    static constexpr int SB = (NB + NW - 1) / NW;
+    static_assert(NA % NW == 0, "A pieces must split evenly over the waves");
+    int a_pix[SA];          // window-origin pixel index (+pshift) of this lane's row in A slot i
+    unsigned a_mask[SA];    // in-bounds 3x3 taps of that row
+    unsigned b_off[SB];
+    unsigned bytes0, bytes1, wbytes;
+    const char *u_src0, *u_src1, *u_wt;   // wave-uniform (SGPR) copies of the kernarg pointers
+    int pshift, tap, cbase, lrow, lchunk;
+    bool two, ctail;
+
+    static constexpr int PMIN = SA + NB / NW, PMAX = SA + SB;
+    // DMA instructions this wave issues per stage (wave-uniform): PMIN or PMAX
+    __device__ __forceinline__ static int pieces(int wave) {
+        return SA + (NB / NW) + (((NB % NW) != 0 && wave < (NB % NW)) ? 1 : 0);
+    }
+    __device__ __forceinline__ int row_of(int wave, int i) const { return (wave + i * NW) * RPP + lrow; }
+    // logical channel chunk this lane fetches so that the lane-linear image is swizzled (lds_sw)
+    __device__ __forceinline__ int chunk_of(int row) const {
+        return (BK == 64 ? (lchunk ^ ((row >> 1) & 7)) : (lchunk ^ ((row >> 2) & 3))) * 8;
+    }
+
+    __device__ __forceinline__ void init(const IgemmParams& p, int m0, int n0, int wave, int lane, int kb) {
+        lrow = lane / CPR;
+        lchunk = lane % CPR;
+        const int hw = p.oh * p.ow;
+        two = p.c1 > 0;
+        pshift = KS == 3 ? p.w + 1 : 0;
+#pragma unroll
+        for (int i = 0; i < SA; ++i) {
+            const int m = m0 + row_of(wave, i);
+            const int mm = m < p.M ? m : 0;
+            const int nn = mm / hw, r = mm - nn * hw;
+            const int oy = r / p.ow, ox = r - oy * p.ow;
+            const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+            unsigned mask = 0;
+            if (m < p.M) {
+#pragma unroll
+                for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+                    for (int kx = 0; kx < KS; ++kx)
+                        if (iy0 + ky >= 0 && iy0 + ky < p.h && ix0 + kx >= 0 && ix0 + kx < p.w)
+                            mask |= 1u << (ky * KS + kx);
+            }
+            a_pix[i] = (nn * p.h + iy0) * p.w + ix0 + pshift;
+            a_mask[i] = mask;
+        }
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            const int row = row_of(wave, i);
+            const int j = n0 + row;
+            b_off[i] = (row < BN && j < p.cout) ? (unsigned)(2 * (j * p.kpad + chunk_of(row))) : kOOB;
+        }
+        const size_t npix = (size_t)p.n * p.h * p.w;
+        bytes0 = (unsigned)(npix * p.c0 * 2);
+        bytes1 = (unsigned)(npix * p.c1 * 2);
+        wbytes = (unsigned)((size_t)p.cout * p.kpad * 2);
+        ctail = (p.cin % BK) != 0;
+        u_src0 = uniform_ptr(p.src0);
+        u_src1 = uniform_ptr(p.src1);
+        u_wt = uniform_ptr(p.wt);
+        cbase = kb * BK;
+        tap = 0;
+        if (KS == 3) { tap = cbase / p.cin; cbase -= tap * p.cin; }
+    }
+
+    // stage K step kt (BK deep) into [A rows | B rows] at lds; steps come in K order
+    __device__ __forceinline__ void issue(const IgemmParams& p, int kt, char* lds, int wave) {
+        const int k0 = kt * BK;
+        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+        const bool use1 = two && cbase >= p.c0;
+        const int cs = use1 ? p.c1 : p.c0;
+        const unsigned sterm = 2u * (unsigned)((KS == 3 ? (ky * p.w + kx) * cs : 0) + (use1 ? cbase - p.c0 : cbase));
+        const char* sb = use1 ? u_src1 : u_src0;
+        const unsigned bias = 2u * (unsigned)(pshift * cs);
+        const unsigned sbytes = use1 ? bytes1 : bytes0;
+        const __amdgpu_buffer_rsrc_t ra = make_rsrc(sb + sterm - bias, sbytes + bias - sterm);
+        const __amdgpu_buffer_rsrc_t rb = make_rsrc(u_wt + 2 * k0, wbytes - 2 * k0);
+        const int lim = p.cin - cbase;
+#pragma unroll
+        for (int i = 0; i < SA; ++i) {
+            const int ch = chunk_of(row_of(wave, i));
+            // branch-free: a dropped tap / channel tail pushes the offset past num_records
+            unsigned ok = (a_mask[i] >> tap) & 1u;
+            if (ctail) ok &= (unsigned)(ch < lim);
+            const unsigned off = (unsigned)(2 * (a_pix[i] * cs + ch)) | ((ok - 1u) & kOOB);
+            dma_piece(ra, lds + (wave + i * NW) * 1024, off);
+        }
+#pragma unroll
+        for (int i = 0; i < SB; ++i) {
+            if (i == SB - 1 && (NB % NW) != 0 && wave >= (NB % NW)) break;   // wave-uniform
+            dma_piece(rb, lds + BM * RB + (wave + i * NW) * 1024, b_off[i]);
+        }
+        cbase += BK;
+        if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
+    }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_c() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (one immediate per case)
+__device__ __forceinline__ void wait_vm(int n) {
+#define C2D_WVM(N) case N: __builtin_amdgcn_s_waitcnt(((N) & 15) | (7 << 4) | (15 << 8) | (((N) >> 4) << 14)); break;
+    switch (n) {
+        C2D_WVM(1) C2D_WVM(2) C2D_WVM(3) C2D_WVM(4) C2D_WVM(5) C2D_WVM(6) C2D_WVM(7) C2D_WVM(8) C2D_WVM(9)
+        C2D_WVM(10) C2D_WVM(11) C2D_WVM(12) C2D_WVM(13) C2D_WVM(14) C2D_WVM(15) C2D_WVM(16) C2D_WVM(18)
+        C2D_WVM(20) C2D_WVM(21) C2D_WVM(24) C2D_WVM(27) C2D_WVM(28) C2D_WVM(30) C2D_WVM(32) C2D_WVM(36)
+        C2D_WVM(40) C2D_WVM(42) C2D_WVM(45) C2D_WVM(48) C2D_WVM(54) C2D_WVM(56) C2D_WVM(60)
+        default: __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8)); break;   // vmcnt(0)
+    }
+#undef C2D_WVM
+}
+
+// LDS-staged epilogue for the 32x32 layout (workgroup LDS free; caller
+// synchronised): accumulators -> fp32 LDS image (tiny unrolled code), then
+// epi_rows (epilogue.h) for bias / activation / GEGLU / temb / residual.
+// Column groups of <= 3 tiles of 32 keep the per-wave image at 32 x 96 fp32.
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x16 (&acc)[TN][TM], int mw0, int nw0,
+                                               int lane, int wave, char* lds) {
+    constexpr int G = TN < 3 ? TN : 3;                       // tiles per column group
+    constexpr int PITCHF = G * 32 + 4;                        // fp32 row pitch (+16 B)
+    float* img = reinterpret_cast<float*>(lds) + wave * 32 * PITCHF;
+    const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+#pragma unroll
+        for (int a0 = 0; a0 < TN; a0 += G) {
+#pragma unroll
+            for (int a = a0; a < a0 + G && a < TN; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+                    *reinterpret_cast<f32x4*>(img + lr * PITCHF + (a - a0) * 32 + g * 8 + lh * 4) = v;
+                }
+            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
+            __builtin_amdgcn_wave_barrier();
+            const int nt = (a0 + G <= TN) ? G : TN - a0;
+            epi_rows(p, img, PITCHF, 32, nt * 32, mw0 + b * 32, nw0 + a0 * 32, lane);
+            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// WM x WN waves, each owning a (TM*32) x (TN*32) output tile (TM row tiles of
+// the activation side, TN column tiles of the weight side): D^T = W . A^T per
+// 32x32 tile.  Per 16-deep k sub-step a wave reads TM + TN fragments
+// (ds_read_b128: lane half h holds k 8h..8h+7 of row lane & 31) for TM*TN MFMAs.
+// Ring: STAGES stages of BK, STAGES-1 in flight; before reading stage kt each
+// wave waits until all but its own younger stages landed (counted vmcnt) and the
+// workgroup passes a raw s_barrier (no vmcnt(0) drain), then re-issues into the
+// slot freed by step kt-1.
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, bool DB>
+__global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) {
+    constexpr int NW = WM * WN;
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int RB = 2 * BK, STAGE = (BM + BN) * RB, NS = BK / 16;
+    typedef M32Loader<BM, BN, BK, NW, KS> Loader;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+    const int bid = xcd_remap(blockIdx.x, p.gx * p.gy * p.ksplit);
+    const int tile = bid / p.ksplit, slice = bid - tile * p.ksplit;
+    const int mt = tile / p.gx, nt = tile - mt * p.gx;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int nk_all = p.kpad / BK;
+    const int kb = slice * p.nkt, ke = min(nk_all, kb + p.nkt);
+    const int per = Loader::pieces(wave);
+
+    Loader ld;
+    ld.init(p, m0, n0, wave, lane, kb);
+
+    int fo[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) fo[s] = lds_sw<BK>(lane & 31, 2 * s + (lane >> 5));
+    const int a_base = wm * TM * 32 * RB, b_base = BM * RB + wn * TN * 32 * RB;
+
+    f32x16 acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+        if (kb + s0 < ke) ld.issue(p, kb + s0, smem + s0 * STAGE, wave);
+    int rd = 0, wr = STAGES - 1;
+    for (int kt = kb; kt < ke; ++kt) {
+        // all but this wave's younger stages in flight (STAGES-2 of them in steady state)
+        if (kt + STAGES - 2 < ke) {
+            if (per == Loader::PMAX) wait_vm_c<Loader::PMAX * (STAGES - 2)>();
+            else wait_vm_c<Loader::PMIN * (STAGES - 2)>();
+        } else {
+            wait_vm(per * (ke - 1 - kt));
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (kt + STAGES - 1 < ke && !(p.abl & 1)) ld.issue(p, kt + STAGES - 1, smem + wr * STAGE, wave);
+        const char* S = smem + rd * STAGE;
+        if (p.abl & 2) {   // timing ablation: fragments read and kept live, no MFMA
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+#pragma unroll
+                for (int t = 0; t < TN; ++t)
+                    asm volatile("" :: "v"(*reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s])));
+#pragma unroll
+                for (int t = 0; t < TM; ++t)
+                    asm volatile("" :: "v"(*reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s])));
+            }
+        } else if (DB) {
+            f16x8 fa[2][TM], fb[2][TN];
+#pragma unroll
+            for (int t = 0; t < TN; ++t) fb[0][t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[0]);
+#pragma unroll
+            for (int t = 0; t < TM; ++t) fa[0][t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[0]);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int cur = s & 1, nxt = cur ^ 1;
+                if (s + 1 < NS) {
+#pragma unroll
+                    for (int t = 0; t < TN; ++t)
+                        fb[nxt][t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s + 1]);
+#pragma unroll
+                    for (int t = 0; t < TM; ++t)
+                        fa[nxt][t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s + 1]);
+                }
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+#pragma unroll
+                    for (int a = 0; a < TN; ++a)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[cur][a], fa[cur][b], acc[a][b], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                f16x8 fa[TM], fb[TN];
+#pragma unroll
+                for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s]);
+#pragma unroll
+                for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s]);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+#pragma unroll
+                    for (int a = 0; a < TN; ++a)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+                __builtin_amdgcn_s_setprio(0);
+            }
+        }
+        rd = (rd + 1 == STAGES) ? 0 : rd + 1;
+        wr = (wr + 1 == STAGES) ? 0 : wr + 1;
+    }
+    const int mw0 = m0 + wm * TM * 32, nw0 = n0 + wn * TN * 32;
+    if (p.ksplit > 1) {
+        float* dst = p.ws + (size_t)slice * p.M * p.cout;
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+            const int m = mw0 + b * 32 + (lane & 31);
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int j = nw0 + a * 32 + g * 8 + 4 * (lane >> 5);
+                    f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+                    if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = v;
+                }
+        }
+        return;
+    }
+    __syncthreads();
+    epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
+}
+
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, bool DB>
+static void launch_m32(const IgemmParams& p, hipStream_t s) {
+    constexpr int smem = STAGES * (WM * TM + WN * TN) * 32 * 2 * BK;
+    static_assert(smem <= 160 * 1024, "LDS ring too large");
+    auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
+    if (p.ksplit > 1) {
+        const size_t total = (size_t)p.M * (p.cout >> 2);
+        const size_t want = (total + 255) / 256;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
+    }
+}
+
+template <int WM, int WN, int TM, int TN, int BK, int ST, bool DB>
+static void run_m32(IgemmParams& p, int ksize, int cout, hipStream_t s) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    p.gx = (cout + BN - 1) / BN;
+    p.gy = (p.M + BM - 1) / BM;
+    p.nkt *= 64 / BK;   // the planner counts 64-deep K steps
+    if (ksize == 1) launch_m32<WM, WN, TM, TN, BK, ST, 1, DB>(p, s);
+    else launch_m32<WM, WN, TM, TN, BK, ST, 3, DB>(p, s);
+}
+
+// ---------------------------------------------------------------------------
+// Ping-pong implicit GEMM (32x32x16 MFMA, BK = 32, 4-stage LDS-DMA ring).
+//
+// The 8 waves form two groups (waves 0-3, 4-7: one wave of each per SIMD).
+// Group 1 runs one barrier behind group 0, so between any two consecutive
+// workgroup barriers one group issues its MFMA cluster while the other issues
+// its LDS fragment reads and DMA: the SIMD's matrix pipe alternates between the
+// two waves it hosts instead of idling while both read LDS.
+//
+// A phase = one 16-deep k sub-step (TM*TN MFMAs).  Per K step kt (2 phases):
+//   phase (kt,0): read frags (kt,1); wait vmcnt -> stage kt+1 landed; B1; MFMA (kt,0); B2
+//   phase (kt,1): read frags (kt+1,0); DMA stage kt+3; B1; MFMA (kt,1); B2
+// Hazards (per wave, with the one-barrier stagger between groups):
+//   RAW  stage kt+1 is read in phase (kt,1), after the B2 of phase (kt,0); every
+//        wave waited for its own pieces before its B1 of phase (kt,0), which for
+//        the other group is at most that same global barrier.
+//   WAR  stage kt+3 overwrites the slot of stage kt-1, whose last fragments were
+//        consumed (lgkmcnt) in the MFMA cluster of phase (kt-1,1), i.e. before
+//        every wave's B2 of (kt-1,1) -- two global barriers earlier.
+template <int WM, int WN, int TM, int TN, int KS>
+__global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
+    constexpr int BK = 32, STAGES = 4;
+    constexpr int NW = WM * WN;
+    static_assert(NW == 8, "two groups of four waves");
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int RB = 2 * BK, STAGE = (BM + BN) * RB;
+    typedef M32Loader<BM, BN, BK, NW, KS> Loader;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2;
+    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+    const int bid = xcd_remap(blockIdx.x, p.gx * p.gy * p.ksplit);
+    const int tile = bid / p.ksplit, slice = bid - tile * p.ksplit;
+    const int mt = tile / p.gx, nt = tile - mt * p.gx;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int nk_all = p.kpad / BK;
+    const int kb = slice * p.nkt, ke = min(nk_all, kb + p.nkt);
+    const int per = Loader::pieces(wave);
+
+    Loader ld;
+    ld.init(p, m0, n0, wave, lane, kb);
+
+    const int fo0 = lds_sw<BK>(lane & 31, lane >> 5), fo1 = lds_sw<BK>(lane & 31, 2 + (lane >> 5));
+    const int a_base = wm * TM * 32 * RB, b_base = BM * RB + wn * TN * 32 * RB;
+
+    f32x16 acc[TN][TM];
+#pragma unroll
+    for (int a = 0; a < TN; ++a)
+#pragma unroll
+        for (int b = 0; b < TM; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+#define C2D_BAR() do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } while (0)
+    f16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+    auto rd_frags = [&](f16x8 (&fa)[TM], f16x8 (&fb)[TN], int stage, int fo) {
+        if (p.abl & 4) return;   // timing ablation: no fragment reads
+        const char* S = smem + (stage & (STAGES - 1)) * STAGE;
+#pragma unroll
+        for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo);
+#pragma unroll
+        for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo);
+    };
+    auto mfma = [&](const f16x8 (&fa)[TM], const f16x8 (&fb)[TN]) {
+        if (p.abl & 2) {   // timing ablation: fragments kept live, no MFMA
+#pragma unroll
+            for (int t = 0; t < TM; ++t) asm volatile("" :: "v"(fa[t]));
+#pragma unroll
+            for (int t = 0; t < TN; ++t) asm volatile("" :: "v"(fb[t]));
+            return;
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int b = 0; b < TM; ++b)
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+    };
+
+    // prologue: stages kb, kb+1, kb+2 in flight; stage kb landed everywhere before the first reads
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+        if (kb + s0 < ke) ld.issue(p, kb + s0, smem + ((kb + s0) & (STAGES - 1)) * STAGE, wave);
+    {
+        const int younger = min(STAGES - 2, ke - 1 - kb);
+        if (younger >= 2 && per == Loader::PMAX) wait_vm_c<2 * Loader::PMAX>();
+        else if (younger >= 2) wait_vm_c<2 * Loader::PMIN>();
+        else wait_vm(per * younger);
+    }
+    C2D_BAR();
+    if (grp) C2D_BAR();   // group 1 runs one barrier behind
+    rd_frags(fa0, fb0, kb, fo0);
+
+    for (int kt = kb; kt < ke; ++kt) {
+        // ---- phase (kt, 0)
+        rd_frags(fa1, fb1, kt, fo1);
+        if (kt + 1 < ke) {   // stage kt+1 landed (stage kt+2 may stay in flight)
+            if (kt + 2 < ke) {
+                if (per == Loader::PMAX) wait_vm_c<Loader::PMAX>();
+                else wait_vm_c<Loader::PMIN>();
+            } else {
+                wait_vm_c<0>();
+            }
+        }
+        C2D_BAR();
+        mfma(fa0, fb0);
+        C2D_BAR();
+        // ---- phase (kt, 1)
+        if (kt + 1 < ke) rd_frags(fa0, fb0, kt + 1, fo0);
+        if (kt + STAGES - 1 < ke && !(p.abl & 1))
+            ld.issue(p, kt + STAGES - 1, smem + ((kt + STAGES - 1) & (STAGES - 1)) * STAGE, wave);
+        C2D_BAR();
+        mfma(fa1, fb1);
+        C2D_BAR();
+    }
+    if (!grp) C2D_BAR();  // balance the stagger before the workgroup ends
+#undef C2D_BAR
+
+    const int mw0 = m0 + wm * TM * 32, nw0 = n0 + wn * TN * 32;
+    if (p.ksplit > 1) {
+        float* dst = p.ws + (size_t)slice * p.M * p.cout;
+#pragma unroll
+        for (int b = 0; b < TM; ++b) {
+            const int m = mw0 + b * 32 + (lane & 31);
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int j = nw0 + a * 32 + g * 8 + 4 * (lane >> 5);
+                    f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+                    if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = v;
+                }
+        }
+        return;
+    }
+    if (p.abl & 8) {   // timing ablation: no epilogue (acc kept live through a never-taken store)
+        float sum = 0.f;
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+            for (int b = 0; b < TM; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sum += acc[a][b][r];
+        if (p.M < 0) p.out[lane] = (f16)sum;
+        return;
+    }
+    __syncthreads();   // every wave is done reading the staging ring
+    epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
+}
+
+template <int WM, int WN, int TM, int TN, int KS>
+static void launch_pp(const IgemmParams& p, hipStream_t s) {
+    constexpr int smem = 4 * (WM * TM + WN * TN) * 32 * 64;
+    static_assert(smem <= 160 * 1024, "LDS ring too large");
+    auto k = igemm_pp_kernel<WM, WN, TM, TN, KS>;
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
+    if (p.ksplit > 1) {
+        const size_t total = (size_t)p.M * (p.cout >> 2);
+        const size_t want = (total + 255) / 256;
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
+    }
+}
+
+template <int WM, int WN, int TM, int TN>
+static void run_pp(IgemmParams& p, int ksize, int cout, hipStream_t s) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    p.gx = (cout + BN - 1) / BN;
+    p.gy = (p.M + BM - 1) / BM;
+    p.nkt *= 2;   // the planner counts 64-deep K steps
+    if (ksize == 1) launch_pp<WM, WN, TM, TN, 1>(p, s);
+    else launch_pp<WM, WN, TM, TN, 3>(p, s);
+}
+
+}  // namespace c2d

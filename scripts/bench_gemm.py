@@ -11,6 +11,7 @@ from clap2diffusion_amd import ops  # noqa: E402
 dev = torch.device("cuda")
 N = 16
 SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)
+    ("L0 k64 64->320", 1, 64, 64, 320),
     ("L0 conv3x3 320", 3, 64, 320, 320),
     ("L1 conv3x3 640", 3, 32, 640, 640),
     ("L2 conv3x3 1280", 3, 16, 1280, 1280),
@@ -51,5 +52,9 @@ def run(name, k, h, cin, cout, iters=20):
     print(f"{name:26s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  relerr {err:.1e}", flush=True)
 
 
+import os
+only = os.environ.get("ONLY")
 for s in SHAPES:
+    if only and not any(o in s[0] for o in only.split(",")):
+        continue
     run(*s)

@@ -58,6 +58,23 @@ def test_conv3x3(dev, n, h, cin, cout, stride, up):
     close(nchw(out), ref)
 
 
+@pytest.mark.parametrize("n,h,cin,cout", [
+    (16, 64, 320, 4),     # UNet conv_out at the bench shape (256x320 tile, 4 live columns)
+    (2, 128, 128, 4),     # VAE conv_out shape class
+    (16, 64, 320, 12),    # width not a multiple of 8: 8-byte epilogue chunks
+])
+def test_conv3x3_narrow_outputs(dev, n, h, cin, cout):
+    x = gen(n, cin, h, h, seed=31)
+    w = gen(cout, cin, 3, 3, seed=32, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=33)
+    resid = gen(n, cout, h, h, seed=34)
+    ref = F.conv2d(x, w, b, padding=1) + resid
+    wp, kp = ops.pack_conv_weight(w)
+    out = ops.conv(nhwc(x).half().to(dev), wp.to(dev), kp, cout, ksize=3, bias=b.float().to(dev),
+                   resid=nhwc(resid).half().to(dev))
+    close(nchw(out), ref)
+
+
 def test_conv3x3_gn_silu_temb_resid(dev):
     n, h, cin, cout, groups = 2, 16, 320, 640, 32
     x = gen(n, cin, h, h, seed=4, scale=2.0) + 0.5
