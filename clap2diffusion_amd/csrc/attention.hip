@@ -20,13 +20,21 @@ template <int D> struct AttnCfg {
     // exactly 16 deep (d = 80), one 16x16x16 MFMA into a separate accumulator
     // (added with VALU: no mixed-shape MFMA accumulation chain) instead of a
     // zero-padded 32 chunk
+    // d < 64 and not a multiple of 32 (d = 40): the whole QK^T on 16x16x16 MFMAs
+    // over 16-deep chunks (K = 48 instead of a zero-padded 64)
+    static constexpr bool C16 = false;   // measured slower on gfx950: 16x16x16 issues at the 16x16x32 cycle count
+    static constexpr int NC16 = C16 ? (D + 15) / 16 : 0;
     static constexpr int NDC = D / 32;
-    static constexpr bool TAIL = (D % 32) == 16;
-    static constexpr int DP = TAIL ? NDC * 32 + 16 : (D + 31) / 32 * 32;
-    static constexpr int NDC_FULL = TAIL ? NDC : DP / 32;  // 32-deep chunks actually issued
+    static constexpr bool TAIL = !C16 && (D % 32) == 16;
+    static constexpr int DP = C16 ? NC16 * 16 : TAIL ? NDC * 32 + 16 : (D + 31) / 32 * 32;
+    static constexpr int NDC_FULL = C16 ? 0 : TAIL ? NDC : DP / 32;  // 32-deep chunks actually issued
     static constexpr int DV = (D + 15) / 16 * 16;      // N dim of PV, multiple of 16
     static constexpr int NDT = DV / 16;
-    static constexpr int KS = DP * 2 + 16;             // K row stride (bytes): odd # of 16-B slots
+    // K rows: 128-B rows with the 16-B chunk XOR swizzle (chunk ^ ((row >> 1) & 7)) when
+    // DP = 64 (conflict-free QK^T fragment reads, PMC-verified need: the padded
+    // 144-B rows measured 2-way conflicts); otherwise rows padded to an odd number of slots
+    static constexpr bool KSW = DP == 64;
+    static constexpr int KS = KSW ? 128 : DP * 2 + 16;
     static constexpr int VS = (DV == 48) ? 96 : (DV == 64 || DV == 80) ? 160 : (DV == 160) ? 352 : DV * 2 + 32;
     static constexpr int DCH = D / 8;                  // real 16-B chunks per row
     static constexpr int NLD = (64 * DCH + 255) / 256; // staged chunks per thread per tile
@@ -34,6 +42,12 @@ template <int D> struct AttnCfg {
     static constexpr int V_BYTES = 64 * VS;
     static constexpr bool SUM_MFMA = DV > D;           // a spare V column carries the row sum
 };
+
+template <int D>
+__device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B chunk ch of K row
+    using C = AttnCfg<D>;
+    return C::KSW ? row * 128 + ((ch ^ ((row >> 1) & 7)) << 4) : row * C::KS + ch * 16;
+}
 
 template <int D, bool MASK>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
@@ -56,7 +70,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
     // zero the K padding columns once (never rewritten) and the V pad columns
     for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 256) {
         int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
-        *reinterpret_cast<f16x8*>(Ks + row * C::KS + ch * 16) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        *reinterpret_cast<f16x8*>(Ks + k_off<D>(row, ch)) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
     }
     // V pad columns: zeros, except column D = 1.0 when there is one, so the PV
     // product also accumulates the softmax row sum (SUM_MFMA)
@@ -71,6 +85,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
     // tail (16x16x16): d = 32 NDC + 4 g .. +3
     f16x8 qf[2][C::NDC_FULL > 0 ? C::NDC_FULL : 1];
     f16x4 qt[2];
+    f16x4 q16[2][C::NC16 > 0 ? C::NC16 : 1];   // C16: d = 16 c + 4 g .. +3
 #pragma unroll
     for (int qg = 0; qg < 2; ++qg) {
         const int qi = q0 + qg * 16 + li;
@@ -81,6 +96,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
                 qf[qg][dc] = *reinterpret_cast<const f16x8*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
             else
                 qf[qg][dc] = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int c = 0; c < C::NC16; ++c) {
+            const int d0 = c * 16 + g * 4;
+            q16[qg][c] = (f16x4){0, 0, 0, 0};
+            if (qi < lq && d0 < D)
+                q16[qg][c] = *reinterpret_cast<const f16x4*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
         }
         qt[qg] = (f16x4){0, 0, 0, 0};
         if (C::TAIL) {
@@ -120,7 +142,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
             const int idx = tid + 256 * i;
             if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
                 const int row = idx / C::DCH, ch = idx - row * C::DCH;
-                *reinterpret_cast<f16x8*>(Ks + row * C::KS + ch * 16) = rk[i];
+                *reinterpret_cast<f16x8*>(Ks + k_off<D>(row, ch)) = rk[i];
                 *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = rv[i];
             }
         }
@@ -145,10 +167,17 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
         for (int kg = 0; kg < 4; ++kg) {
 #pragma unroll
             for (int dc = 0; dc < C::NDC_FULL; ++dc) {
-                const f16x8 kf = *reinterpret_cast<const f16x8*>(Ks + (kg * 16 + li) * C::KS + (dc * 4 + g) * 16);
+                const f16x8 kf = *reinterpret_cast<const f16x8*>(Ks + k_off<D>(kg * 16 + li, dc * 4 + g));
 #pragma unroll
                 for (int qg = 0; qg < 2; ++qg)
                     s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], s[qg][kg], 0, 0, 0);
+            }
+#pragma unroll
+            for (int c = 0; c < C::NC16; ++c) {
+                const f16x4 kt = *reinterpret_cast<const f16x4*>(Ks + (kg * 16 + li) * C::KS + c * 32 + g * 8);
+#pragma unroll
+                for (int qg = 0; qg < 2; ++qg)
+                    s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x16f16(kt, q16[qg][c], s[qg][kg], 0, 0, 0);
             }
             if (C::TAIL) {
                 const f16x4 kt = *reinterpret_cast<const f16x4*>(Ks + (kg * 16 + li) * C::KS + C::NDC * 64 + g * 8);

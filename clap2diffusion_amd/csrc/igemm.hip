@@ -712,13 +712,8 @@ struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
 static const DmaTile kDmaTiles[] = {
     // 32x32x16 MFMA, deep LDS-DMA ring (igemm_m32.h); rate 0 = only when forced (C2D_GEMM_TILE)
     {20, 256, 320, 1, 0.0f, true},
-    {21, 256, 256, 1, 0.0f, true},
-    {22, 128, 320, 1, 0.0f, true},
     {23, 256, 320, 1, 0.0f, true},
-    {24, 128, 256, 1, 0.0f, true},
     {30, 256, 320, 1, 0.0f, true},
-    {31, 128, 320, 1, 0.0f, true},
-    {32, 256, 256, 1, 0.0f, true},
     {7, 128, 320, 1, 3.1f, false},
     {1, 256, 128, 1, 2.9f, true},
     {2, 128, 128, 1, 2.2f, true},
@@ -797,14 +792,9 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
     switch (pl.id) {
-        case 20: return run_m32<4, 2, 2, 5, 32, 4, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160
-        case 21: return run_m32<4, 2, 2, 4, 32, 4, true>(p, ksize, cout, s);   // 256x256, 8 waves of 64x128
-        case 22: return run_m32<4, 2, 1, 5, 32, 4, true>(p, ksize, cout, s);   // 128x320, 8 waves of 32x160
-        case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, BK 64, 2 stages
-        case 24: return run_m32<2, 2, 2, 4, 32, 6, true>(p, ksize, cout, s);   // 128x256, 4 waves of 64x128
+        case 20: return run_m32<4, 2, 2, 5, 32, 4, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 32
+        case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 64
         case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
-        case 31: return run_pp<4, 2, 1, 5>(p, ksize, cout, s);   // 128x320 ping-pong, 8 waves of 32x160
-        case 32: return run_pp<4, 2, 2, 4>(p, ksize, cout, s);   // 256x256 ping-pong, 8 waves of 64x128
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
         case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64
         case 2: return run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s);   // 128x128, 4 waves of 64x64

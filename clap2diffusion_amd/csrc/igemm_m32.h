@@ -353,21 +353,25 @@ static void run_m32(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 // Ping-pong implicit GEMM (32x32x16 MFMA, BK = 32, 4-stage LDS-DMA ring).
 //
 // The 8 waves form two groups (waves 0-3, 4-7: one wave of each per SIMD).
-// Group 1 runs one barrier behind group 0, so between any two consecutive
+// Group 1 runs one barrier behind group 0, so between two consecutive
 // workgroup barriers one group issues its MFMA cluster while the other issues
-// its LDS fragment reads and DMA: the SIMD's matrix pipe alternates between the
-// two waves it hosts instead of idling while both read LDS.
+// its LDS fragment reads (and DMA): the SIMD's matrix pipe alternates between
+// the two waves it hosts instead of idling while both read LDS.  Fragments are
+// single-buffered (the overlap is across the two waves of a SIMD, not inside a
+// wave), which keeps the 160 accumulator registers of a 64x160 wave tile
+// spill-free.
 //
-// A phase = one 16-deep k sub-step (TM*TN MFMAs).  Per K step kt (2 phases):
-//   phase (kt,0): read frags (kt,1); wait vmcnt -> stage kt+1 landed; B1; MFMA (kt,0); B2
-//   phase (kt,1): read frags (kt+1,0); DMA stage kt+3; B1; MFMA (kt,1); B2
-// Hazards (per wave, with the one-barrier stagger between groups):
-//   RAW  stage kt+1 is read in phase (kt,1), after the B2 of phase (kt,0); every
-//        wave waited for its own pieces before its B1 of phase (kt,0), which for
-//        the other group is at most that same global barrier.
-//   WAR  stage kt+3 overwrites the slot of stage kt-1, whose last fragments were
-//        consumed (lgkmcnt) in the MFMA cluster of phase (kt-1,1), i.e. before
-//        every wave's B2 of (kt-1,1) -- two global barriers earlier.
+// A phase = one 16-deep k sub-step (TM*TN MFMAs), two per K step kt:
+//   phase (kt,0): read frags (kt,0);                                   B1; MFMA; B2
+//   phase (kt,1): DMA stage kt+3; read frags (kt,1); wait stage kt+1;   B1; MFMA; B2
+// Hazards, with the one-barrier stagger between the groups:
+//   RAW  stage kt+1 is first read in phase (kt+1,0), after this wave's B2 of
+//        (kt,1); every wave waited for its own pieces of stage kt+1 before its
+//        B1 of (kt,1), which for the other group is at most that barrier.
+//   WAR  the DMA of stage kt+3 (phase (kt,1), after this wave's B2 of (kt,0))
+//        overwrites the slot of stage kt-1, whose last fragments every wave
+//        consumed (lgkmcnt) before its B2 of (kt-1,1): at least one global
+//        barrier earlier for either group.
 template <int WM, int WN, int TM, int TN, int KS>
 __global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
     constexpr int BK = 32, STAGES = 4;
@@ -405,8 +409,8 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
 #define C2D_BAR() do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } while (0)
-    f16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
-    auto rd_frags = [&](f16x8 (&fa)[TM], f16x8 (&fb)[TN], int stage, int fo) {
+    f16x8 fa[TM], fb[TN];
+    auto rd_frags = [&](int stage, int fo) {
         if (p.abl & 4) return;   // timing ablation: no fragment reads
         const char* S = smem + (stage & (STAGES - 1)) * STAGE;
 #pragma unroll
@@ -414,7 +418,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
 #pragma unroll
         for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo);
     };
-    auto mfma = [&](const f16x8 (&fa)[TM], const f16x8 (&fb)[TN]) {
+    auto mfma = [&]() {
         if (p.abl & 2) {   // timing ablation: fragments kept live, no MFMA
 #pragma unroll
             for (int t = 0; t < TM; ++t) asm volatile("" :: "v"(fa[t]));
@@ -430,41 +434,40 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
     };
+    // vmcnt(per * n) for n = 0, 1, 2 younger stages of this wave in flight
+    auto wait_younger = [&](int n) {
+        if (n >= 2) {
+            if (per == Loader::PMAX) wait_vm_c<2 * Loader::PMAX>();
+            else wait_vm_c<2 * Loader::PMIN>();
+        } else if (n == 1) {
+            if (per == Loader::PMAX) wait_vm_c<Loader::PMAX>();
+            else wait_vm_c<Loader::PMIN>();
+        } else {
+            wait_vm_c<0>();
+        }
+    };
 
-    // prologue: stages kb, kb+1, kb+2 in flight; stage kb landed everywhere before the first reads
+    // prologue: stages kb..kb+2 in flight, stage kb landed everywhere before the first read
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
         if (kb + s0 < ke) ld.issue(p, kb + s0, smem + ((kb + s0) & (STAGES - 1)) * STAGE, wave);
-    {
-        const int younger = min(STAGES - 2, ke - 1 - kb);
-        if (younger >= 2 && per == Loader::PMAX) wait_vm_c<2 * Loader::PMAX>();
-        else if (younger >= 2) wait_vm_c<2 * Loader::PMIN>();
-        else wait_vm(per * younger);
-    }
+    wait_younger(min(2, ke - 1 - kb));
     C2D_BAR();
     if (grp) C2D_BAR();   // group 1 runs one barrier behind
-    rd_frags(fa0, fb0, kb, fo0);
 
     for (int kt = kb; kt < ke; ++kt) {
         // ---- phase (kt, 0)
-        rd_frags(fa1, fb1, kt, fo1);
-        if (kt + 1 < ke) {   // stage kt+1 landed (stage kt+2 may stay in flight)
-            if (kt + 2 < ke) {
-                if (per == Loader::PMAX) wait_vm_c<Loader::PMAX>();
-                else wait_vm_c<Loader::PMIN>();
-            } else {
-                wait_vm_c<0>();
-            }
-        }
+        rd_frags(kt, fo0);
         C2D_BAR();
-        mfma(fa0, fb0);
+        mfma();
         C2D_BAR();
         // ---- phase (kt, 1)
-        if (kt + 1 < ke) rd_frags(fa0, fb0, kt + 1, fo0);
         if (kt + STAGES - 1 < ke && !(p.abl & 1))
             ld.issue(p, kt + STAGES - 1, smem + ((kt + STAGES - 1) & (STAGES - 1)) * STAGE, wave);
+        rd_frags(kt, fo1);
+        if (kt + 1 < ke) wait_younger((kt + 2 < ke) + (kt + 3 < ke));   // stage kt+1 landed
         C2D_BAR();
-        mfma(fa1, fb1);
+        mfma();
         C2D_BAR();
     }
     if (!grp) C2D_BAR();  // balance the stagger before the workgroup ends
@@ -485,17 +488,6 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
                     if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = v;
                 }
         }
-        return;
-    }
-    if (p.abl & 8) {   // timing ablation: no epilogue (acc kept live through a never-taken store)
-        float sum = 0.f;
-#pragma unroll
-        for (int a = 0; a < TN; ++a)
-#pragma unroll
-            for (int b = 0; b < TM; ++b)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sum += acc[a][b][r];
-        if (p.M < 0) p.out[lane] = (f16)sum;
         return;
     }
     __syncthreads();   // every wave is done reading the staging ring
