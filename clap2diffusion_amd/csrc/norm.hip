@@ -96,11 +96,14 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
     }
 }
 
-// grid (n, group chunks): a block owns gpb = 256 / cpg whole groups of one image.
-// Thread t sums channel (c_begin + t)'s per-block moments over the nblk partial
-// blocks (coalesced float2 loads, fixed order, fp64); each group then folds its
-// cpg channel totals in fixed order -> mean / rstd -> the per-(image, channel)
-// affine tables.
+// threads per channel in the finalize: 4 for up to 64 channels per group
+__host__ __device__ inline int gn_tpc(int cpg) { return cpg <= 64 ? 4 : (cpg <= 128 ? 2 : 1); }
+
+// grid (n, group chunks): a block owns gpb = 256 / (cpg * tpc) whole groups of one
+// image.  tpc threads per channel each sum every tpc-th per-block moment (coalesced
+// float2 loads, fixed order, fp64) and combine by a fixed xor butterfly; each group
+// then folds its cpg channel totals in fixed order -> mean / rstd -> the
+// per-(image, channel) affine tables.  Deterministic, no atomics.
 __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
                                                           int c0, int c1, int hw, int groups, int nblk, float eps,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -109,30 +112,38 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict_
     __shared__ double csum[256], csq[256];
     __shared__ float g_mean[256], g_rstd[256];
     const int cin = c0 + c1, cpg = cin / groups;
-    const int gpb = 256 / cpg;
+    const int tpc = gn_tpc(cpg);
+    const int gpb = 256 / (cpg * tpc);
     const int n = blockIdx.x, g0 = blockIdx.y * gpb;
     const int ng = min(gpb, groups - g0);
     const int c_begin = g0 * cpg, nc = ng * cpg;
     const int t = threadIdx.x;
+    const int cs = t / tpc, part = t - cs * tpc;
     const size_t img = (size_t)n * hw;
-    const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * cin + c_begin + t;
-    if (t < nc) {
-        double a = 0.0, b = 0.0;
-        int blk = 0;
-        for (; blk + 4 <= nblk; blk += 4) {
-            const float2 v0 = wp[(size_t)(blk + 0) * cin], v1 = wp[(size_t)(blk + 1) * cin];
-            const float2 v2 = wp[(size_t)(blk + 2) * cin], v3 = wp[(size_t)(blk + 3) * cin];
+    const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * cin + c_begin + (cs < nc ? cs : 0);
+    double a = 0.0, b = 0.0;
+    if (cs < nc) {
+        int blk = part;
+        for (; blk + 3 * tpc < nblk; blk += 4 * tpc) {
+            const float2 v0 = wp[(size_t)blk * cin], v1 = wp[(size_t)(blk + tpc) * cin];
+            const float2 v2 = wp[(size_t)(blk + 2 * tpc) * cin], v3 = wp[(size_t)(blk + 3 * tpc) * cin];
             a += (double)v0.x; b += (double)v0.y;
             a += (double)v1.x; b += (double)v1.y;
             a += (double)v2.x; b += (double)v2.y;
             a += (double)v3.x; b += (double)v3.y;
         }
-        for (; blk < nblk; ++blk) {
+        for (; blk < nblk; blk += tpc) {
             const float2 v = wp[(size_t)blk * cin];
             a += (double)v.x; b += (double)v.y;
         }
-        csum[t] = a;
-        csq[t] = b;
+    }
+    for (int o = 1; o < tpc; o <<= 1) {   // tpc divides 64: a channel's threads share a wave
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
+    }
+    if (cs < nc && part == 0) {
+        csum[cs] = a;
+        csq[cs] = b;
     }
     __syncthreads();
     if (t < ng) {
@@ -304,7 +315,7 @@ extern "C" int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, i
         hipLaunchKernelGGL((gn_partial_kernel<2>), grid, dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1,
                            hw, cpg, rows_per_block, (float*)ws);
     }
-    const int gpb = 256 / cpg;
+    const int gpb = 256 / (cpg * gn_tpc(cpg));
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(n, (groups + gpb - 1) / gpb), dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, c1, hw,
                        groups, nblk, eps, gamma, beta, (const float*)ws, scale, shift);
     return check_launch();
