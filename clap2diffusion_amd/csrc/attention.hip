@@ -12,6 +12,7 @@
 // LDS read).  O^T accumulators keep the query on the lane, so the online-softmax
 // rescale is lane-local.  Softmax in fp32 with exp2 and a folded log2(e) scale.
 #include "common.h"
+#include <stdlib.h>
 
 namespace c2d {
 
@@ -301,6 +302,258 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
     }
 }
 
+// ---------------------------------------------------------------------------
+// Software-pipelined variant for d <= 64 (DP = 64: d = 40, 64).  Same fragment
+// layouts as attn_fwd_kernel, but K/V tiles are double-buffered in LDS and each
+// iteration issues the QK^T MFMAs of tile t+1 and the PV MFMAs of tile t, with
+// the softmax of tile t+1 (VALU: max, exp2, pack) placed between the PV MFMAs so
+// a wave's matrix and vector pipes overlap (the d = 40 kernel is exp-bound: PMC
+// showed MFMA ~40 % and VALU ~47 % busy, executed back to back).  The online-
+// softmax rescale of tile t+1 is applied after the PV of tile t retires.
+template <int D, bool MASK>
+__global__ void __launch_bounds__(256) attn_pp_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
+                                                      int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
+                                                      int ldo, int heads, int lq, int lk, float scale_log2,
+                                                      int kv_div, int nqb) {
+    using C = AttnCfg<D>;
+    static_assert(C::KSW && C::NDC_FULL == 2 && !C::TAIL, "pipelined attention: DP = 64 only");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // buffer bb: K at smem + bb * K_BYTES, V at smem + 2 * K_BYTES + bb * V_BYTES
+#define KB(bb) (smem + (bb) * C::K_BYTES)
+#define VB(bb) (smem + 2 * C::K_BYTES + (bb) * C::V_BYTES)
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int bh = tile / nqb, qb = tile - bh * nqb;
+    const int b = bh / heads, h = bh - b * heads;
+    const int bk = b / kv_div;
+    const int q0 = qb * 128 + wave * 32;
+    const int g = lane >> 4, li = lane & 15;
+
+    // pads of both buffers: K chunks >= DCH zero; V pad columns zero except the ones column at D
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+        for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 256) {
+            const int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
+            *reinterpret_cast<f16x8*>(KB(bb) + k_off<D>(row, ch)) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 256) {
+            const int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
+            f16x8 z = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+            if (ch == C::DCH) z[0] = (f16)1.0f;
+            *reinterpret_cast<f16x8*>(VB(bb) + row * C::VS + ch * 16) = z;
+        }
+    }
+
+    f16x8 qf[2][2];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+        const int qi = q0 + qg * 16 + li;
+#pragma unroll
+        for (int dc = 0; dc < 2; ++dc) {
+            const int d0 = dc * 32 + g * 8;
+            if (qi < lq && d0 < D)
+                qf[qg][dc] = *reinterpret_cast<const f16x8*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
+            else
+                qf[qg][dc] = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    f32x4 acc[C::NDT][2];
+#pragma unroll
+    for (int dt = 0; dt < C::NDT; ++dt)
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) acc[dt][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float m_run[2] = {-1e30f, -1e30f};
+
+    const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
+    const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
+    f16x8 rk[C::NLD], rv[C::NLD];
+    auto gload = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            const int idx = tid + 256 * i;
+            const int row = idx / C::DCH, ch = idx - row * C::DCH;
+            const int key = min(t * 64 + row, lk - 1);   // past lk: masked scores, P = 0
+            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
+                rk[i] = *reinterpret_cast<const f16x8*>(kbase + (size_t)key * ldk + ch * 8);
+                rv[i] = *reinterpret_cast<const f16x8*>(vbase + (size_t)key * ldv + ch * 8);
+            }
+        }
+    };
+    auto swrite = [&](int bb) {
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            const int idx = tid + 256 * i;
+            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
+                const int row = idx / C::DCH, ch = idx - row * C::DCH;
+                *reinterpret_cast<f16x8*>(KB(bb) + k_off<D>(row, ch)) = rk[i];
+                *reinterpret_cast<f16x8*>(VB(bb) + row * C::VS + ch * 16) = rv[i];
+            }
+        }
+    };
+    // S^T tiles of K tile in buffer bb: s[qg][kg] = keys 16 kg + 4 g + r of query li
+    auto qk = [&](f32x4 (&s)[2][4], int bb) {
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg) s[qg][kg] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+            for (int dc = 0; dc < 2; ++dc) {
+                const f16x8 kf = *reinterpret_cast<const f16x8*>(KB(bb) + k_off<D>(kg * 16 + li, dc * 4 + g));
+#pragma unroll
+                for (int qg = 0; qg < 2; ++qg)
+                    s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], s[qg][kg], 0, 0, 0);
+            }
+    };
+    // online softmax of one tile (log2 domain, lazy 2^8 rescale): P fragments + the
+    // per-query-group rescale factor to apply to O once the previous PV retired
+    auto softmax = [&](f32x4 (&s)[2][4], f16x8 (&pf)[2][2], float (&alpha)[2], int t) {
+        if (MASK && (t + 1) * 64 > lk) {
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = t * 64 + kg * 16 + g * 4 + r;
+                    if (key >= lk) { s[0][kg][r] = -1e30f; s[1][kg][r] = -1e30f; }
+                }
+        }
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) {
+            float mx = s[qg][0][0];
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qg][kg][r]);
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            // branch-free lazy rescale (keeps the pipelined block one scheduling region)
+            const float m_cand = fmaxf(m_run[qg], mx * scale_log2);
+            const bool up = __builtin_amdgcn_ballot_w64(m_cand > m_run[qg] + 8.0f) != 0;
+            const float m_new = up ? m_cand : m_run[qg];
+            alpha[qg] = __builtin_amdgcn_exp2f(m_run[qg] - m_new);
+            m_run[qg] = m_new;
+            const float m_use = m_new;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    pf[qg][kb][j] = (f16)__builtin_amdgcn_exp2f(fmaf(s[qg][2 * kb][j], scale_log2, -m_use));
+                    pf[qg][kb][4 + j] = (f16)__builtin_amdgcn_exp2f(fmaf(s[qg][2 * kb + 1][j], scale_log2, -m_use));
+                }
+        }
+    };
+    // O^T += V^T P^T for the V tile in buffer bb
+    auto pv = [&](const f16x8 (&pf)[2][2], int bb) {
+#pragma unroll
+        for (int dt = 0; dt < C::NDT; ++dt)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const int qq = li >> 2, pp = li & 3;
+                const int row1 = kb * 32 + g * 4 + qq;
+                const char* a1 = VB(bb) + row1 * C::VS + (dt * 16 + pp * 4) * 2;
+                const char* a2 = a1 + 16 * C::VS;
+                s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a1);
+                s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a2);
+                f16x8 vf;
+                f16x4 h1 = __builtin_bit_cast(f16x4, t1), h2 = __builtin_bit_cast(f16x4, t2);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { vf[j] = h1[j]; vf[4 + j] = h2[j]; }
+#pragma unroll
+                for (int qg = 0; qg < 2; ++qg)
+                    acc[dt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[qg][kb], acc[dt][qg], 0, 0, 0);
+            }
+    };
+
+    const int ntiles = (lk + 63) / 64;
+    // prologue: tiles 0 and 1 staged, softmax of tile 0 done, tile 2 in registers
+    gload(0);
+    __syncthreads();   // pad zeroing done
+    swrite(0);
+    if (ntiles > 1) { gload(1); swrite(1); }
+    __syncthreads();
+    if (ntiles > 2) gload(2);
+    f16x8 pcur[2][2], pnxt[2][2];
+    {
+        f32x4 s0[2][4];
+        float a0[2];
+        qk(s0, 0);
+        softmax(s0, pcur, a0, 0);   // acc is zero: no rescale needed
+    }
+    for (int t = 0; t < ntiles; ++t) {
+        const int cb = t & 1;
+        if (t + 1 < ntiles) {
+            f32x4 sn[2][4];
+            float an[2];
+            qk(sn, cb ^ 1);             // MFMA: scores of tile t+1
+            pv(pcur, cb);               // MFMA: O += P(t) V(t)
+            softmax(sn, pnxt, an, t + 1);   // VALU, overlaps the PV MFMAs in flight
+            // interleave: K-fragment reads + QK^T MFMAs, then each PV MFMA (with its
+            // two transposed V reads) followed by a slice of the softmax VALU work
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+            }
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+                for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= an[qg];
+#pragma unroll
+            for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) pcur[qg][kb] = pnxt[qg][kb];
+        } else {
+            pv(pcur, cb);
+        }
+        if (t + 2 < ntiles) {
+            __syncthreads();            // every wave is done with buffer cb (K(t), V(t))
+            swrite(cb);                 // tile t+2
+            __syncthreads();
+            if (t + 3 < ntiles) gload(t + 3);
+        }
+    }
+
+    // epilogue: lane holds O[query li][d = 16 dt + 4 g + r]; row sum in the ones column D
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+        const float l = __shfl(acc[D / 16][qg][D % 4], li + 16 * ((D % 16) / 4));
+        const float inv = 1.0f / l;
+        const int qi = q0 + qg * 16 + li;
+        if (qi >= lq) continue;
+        f16* orow = o + ((size_t)b * lq + qi) * ldo + h * D;
+#pragma unroll
+        for (int dt = 0; dt < C::NDT; ++dt) {
+            const int d0 = dt * 16 + g * 4;
+            if (d0 < D) {
+                f16x4 ov;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ov[r] = (f16)(acc[dt][qg][r] * inv);
+                *reinterpret_cast<f16x4*>(orow + d0) = ov;
+            }
+        }
+    }
+}
+
+#undef KB
+#undef VB
+
+// C2D_ATTN_PP=1 selects the double-buffered, software-pipelined d=40 kernel.  Measured
+// slower than the single-buffered one on MI355X (L0 self 4096x4096: 779 vs 653 us): the
+// in-flight S tile takes it to 148 VGPR + 24 AGPR = 2 waves/SIMD vs 126 + 40 = 3 for
+// attn_fwd_kernel<40>, and the doubled K/V ring halves the blocks LDS admits, so it is
+// off by default.
+static int attn_pipelined() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
 template <int D>
 static int launch_attn(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                        int batch, int heads, int lq, int lk, float scale, int kv_div, hipStream_t s) {
@@ -308,6 +561,20 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
     const int nqb = (lq + 127) / 128;
     const int smem = C::K_BYTES + C::V_BYTES;
     dim3 grid(nqb * batch * heads);
+    if constexpr (C::KSW && C::SUM_MFMA) {
+        if (attn_pipelined()) {
+            const int smem2 = 2 * (C::K_BYTES + C::V_BYTES);
+            if (lk % 64 == 0)
+                hipLaunchKernelGGL((attn_pp_kernel<D, false>), grid, dim3(256), smem2, s, (const f16*)q, ldq,
+                                   (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk,
+                                   scale * 1.4426950408889634f, kv_div, nqb);
+            else
+                hipLaunchKernelGGL((attn_pp_kernel<D, true>), grid, dim3(256), smem2, s, (const f16*)q, ldq,
+                                   (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk,
+                                   scale * 1.4426950408889634f, kv_div, nqb);
+            return check_launch();
+        }
+    }
     if (lk % 64 == 0)
         hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
                            (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
