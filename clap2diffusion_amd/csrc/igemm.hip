@@ -39,6 +39,7 @@ struct IgemmParams {
     float* ws;   // split-K fp32 partials [ksplit][M][cout]
     int abl;     // timing ablation bits (C2D_GEMM_ABL; 0 in production)
     int lds_epi; // 32x32 kernels: LDS-staged coalesced epilogue (C2D_GEMM_LDSEPI, default on)
+    int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_GEMM_KORDER, default 1)
 };
 
 }  // namespace c2d
@@ -486,10 +487,15 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     const char* u_src0 = uniform_ptr(p.src0);
     const char* u_src1 = uniform_ptr(p.src1);
     const char* u_wt = uniform_ptr(p.wt);
-    int tap = 0, cbase = kb * 64;                                 // (tap, channel block) of the next issue
-    if (KS == 3) { tap = cbase / p.cin; cbase -= tap * p.cin; }
+    // (tap, channel block) of the next issue; the packed weight column is tap * cin + cbase
+    int tap = 0, cbase = kb * 64;
+    if (KS == 3) {
+        if (p.cmajor) { tap = kb % 9; cbase = (kb / 9) * 64; }
+        else { tap = cbase / p.cin; cbase -= tap * p.cin; }
+    }
     auto issue = [&](int kt, int buf) {
-        const int k0 = kt * 64;
+        (void)kt;
+        const int k0 = tap * p.cin + cbase;
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
         const bool use1 = two && cbase >= p.c0;
         const int cs = use1 ? p.c1 : p.c0;
@@ -512,8 +518,12 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
 #pragma unroll
         for (int i = 0; i < BI; ++i)
             dma_piece(rb, base + A_BYTES + (wave * BI + i) * 1024, b_off[i]);
-        cbase += 64;                                               // issues come in K order
-        if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
+        if (KS == 3 && p.cmajor) {                                 // taps inner
+            if (++tap == 9) { tap = 0; cbase += 64; }
+        } else {                                                   // packed K order
+            cbase += 64;
+            if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
+        }
     };
 
     // ---- fragment read offsets: tile t of this wave = base + t * 2 KiB (the swizzle
@@ -753,6 +763,17 @@ static int gemm_abl() {
     return v;
 }
 
+// K-step order of the 3x3 DMA kernels.  1 (default): for each 64-channel block all
+// 9 taps, so one block re-reads a (rows + 2 halo image rows) x 64-channel slab from
+// L2 nine times in a row (~1.6 MB live per XCD at 32 resident 256-row blocks).
+// 0: tap-major, the packed weight order, whose reuse distance (rows x cin) spills
+// the 4 MB L2 at cin = 320 and re-fetches the input over the fabric once per tap.
+static int gemm_korder() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GEMM_KORDER"); v = e ? atoi(e) : 1; }
+    return v;
+}
+
 static int gemm_lds_epi() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_GEMM_LDSEPI"); v = e ? atoi(e) : 1; }
@@ -873,6 +894,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.ws = nullptr;
     p.abl = gemm_abl();
     p.lds_epi = gemm_lds_epi();
+    p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
         DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act);

@@ -99,12 +99,16 @@ struct M32Loader {
         u_wt = uniform_ptr(p.wt);
         cbase = kb * BK;
         tap = 0;
-        if (KS == 3) { tap = cbase / p.cin; cbase -= tap * p.cin; }
+        if (KS == 3) {
+            if (p.cmajor) { tap = kb % 9; cbase = (kb / 9) * BK; }
+            else { tap = cbase / p.cin; cbase -= tap * p.cin; }
+        }
     }
 
-    // stage K step kt (BK deep) into [A rows | B rows] at lds; steps come in K order
+    // stage K step kt (BK deep) into [A rows | B rows] at lds; steps come in the order init/issue advance (tap, cbase)
     __device__ __forceinline__ void issue(const IgemmParams& p, int kt, char* lds, int wave) {
-        const int k0 = kt * BK;
+        (void)kt;
+        const int k0 = tap * p.cin + cbase;              // packed weight column of this step
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
         const bool use1 = two && cbase >= p.c0;
         const int cs = use1 ? p.c1 : p.c0;
@@ -129,8 +133,12 @@ struct M32Loader {
             if (i == SB - 1 && (NB % NW) != 0 && wave >= (NB % NW)) break;   // wave-uniform
             dma_piece(rb, lds + BM * RB + (wave + i * NW) * 1024, b_off[i]);
         }
-        cbase += BK;
-        if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
+        if (KS == 3 && p.cmajor) {                        // taps inner (C2D_GEMM_KORDER)
+            if (++tap == 9) { tap = 0; cbase += BK; }
+        } else {
+            cbase += BK;
+            if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
+        }
     }
 };
 
