@@ -16,6 +16,7 @@
 // into a double-buffered, XOR-swizzled LDS image: one barrier per K step.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace c2d {
 
@@ -723,6 +724,9 @@ static const DmaTile kDmaTiles[] = {
     // 32x32x16 MFMA, deep LDS-DMA ring (igemm_m32.h); rate 0 = only when forced (C2D_GEMM_TILE)
     {20, 256, 320, 1, 0.0f, true},
     {23, 256, 320, 1, 0.0f, true},
+    {21, 256, 320, 1, 0.0f, true},
+    {24, 256, 320, 1, 0.0f, true},
+    {26, 128, 320, 1, 0.0f, true},
     {30, 256, 320, 1, 0.0f, true},
     {7, 128, 320, 1, 3.1f, false},
     {1, 256, 128, 1, 2.9f, true},
@@ -802,8 +806,15 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
         DmaPlan pl = plan_dma(M, cout, nk, geglu, id, gemm_split());
         if (pl.id) return pl;
     }
-    const long t23 = ((M + 255) / 256) * ((cout + 319) / 320);
-    if (t23 >= 256) return {23, 1, nk};
+    // rules from the shape sweeps (scripts/sweep_tiles.sh): the 256x320 interleaved-DMA
+    // tile once it (nearly) fills the chip, and with split-K for the long-K convs
+    // (9 * cin >= 5760: L1 / L2 resnet and up-block convs); 128x320 below that
+    const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
+    if (t24 >= 192) return {24, 1, nk};
+    if (nk >= 90 && t24 >= 64) {
+        DmaPlan pl = plan_dma(M, cout, nk, geglu, 24, 0);
+        if (pl.id) return pl;
+    }
     const long t7 = geglu ? ((M + 255) / 256) * ((cout + 127) / 128) : ((M + 127) / 128) * ((cout + 319) / 320);
     if (t7 >= 256) return {geglu ? 1 : 7, 1, nk};
     return plan_dma(M, cout, nk, geglu, 0, 0);
@@ -815,6 +826,9 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     switch (pl.id) {
         case 20: return run_m32<4, 2, 2, 5, 32, 4, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 32
         case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 64
+        case 21: return run_m32<4, 2, 2, 5, 32, 4, 2>(p, ksize, cout, s);      // as 20, DMA interleaved with MFMAs
+        case 24: return run_m32<4, 2, 2, 5, 64, 2, 2>(p, ksize, cout, s);      // as 23, DMA interleaved with MFMAs
+        case 26: return run_m32<4, 2, 1, 5, 32, 5, 2>(p, ksize, cout, s);      // 128x320, 8 waves of 32x160, BK 32
         case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
         case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64

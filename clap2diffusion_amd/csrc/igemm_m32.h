@@ -44,8 +44,8 @@ struct M32Loader {
     unsigned b_off[SB];
     unsigned bytes0, bytes1, wbytes;
     const char *u_src0, *u_src1, *u_wt;   // wave-uniform (SGPR) copies of the kernarg pointers
-    int pshift, tap, cbase, lrow, lchunk;
-    bool two, ctail;
+    int pshift, tap, cbase, lrow, lchunk, cin_;
+    bool two, ctail, cbase_major;
 
     static constexpr int PMIN = SA + NB / NW, PMAX = SA + SB;
     // DMA instructions this wave issues per stage (wave-uniform): PMIN or PMAX
@@ -94,6 +94,8 @@ struct M32Loader {
         bytes1 = (unsigned)(npix * p.c1 * 2);
         wbytes = (unsigned)((size_t)p.cout * p.kpad * 2);
         ctail = (p.cin % BK) != 0;
+        cin_ = p.cin;
+        cbase_major = p.cmajor != 0;
         u_src0 = uniform_ptr(p.src0);
         u_src1 = uniform_ptr(p.src1);
         u_wt = uniform_ptr(p.wt);
@@ -105,40 +107,58 @@ struct M32Loader {
         }
     }
 
-    // stage K step kt (BK deep) into [A rows | B rows] at lds; steps come in the order init/issue advance (tap, cbase)
-    __device__ __forceinline__ void issue(const IgemmParams& p, int kt, char* lds, int wave) {
-        (void)kt;
+    // per-stage wave-uniform part of the addressing (descriptors in SGPRs)
+    struct Stage {
+        __amdgpu_buffer_rsrc_t ra, rb;
+        int cs, lim;
+    };
+    __device__ __forceinline__ Stage prep(const IgemmParams& p) const {
+        Stage st;
         const int k0 = tap * p.cin + cbase;              // packed weight column of this step
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
         const bool use1 = two && cbase >= p.c0;
-        const int cs = use1 ? p.c1 : p.c0;
-        const unsigned sterm = 2u * (unsigned)((KS == 3 ? (ky * p.w + kx) * cs : 0) + (use1 ? cbase - p.c0 : cbase));
+        st.cs = use1 ? p.c1 : p.c0;
+        const unsigned sterm = 2u * (unsigned)((KS == 3 ? (ky * p.w + kx) * st.cs : 0) + (use1 ? cbase - p.c0 : cbase));
         const char* sb = use1 ? u_src1 : u_src0;
-        const unsigned bias = 2u * (unsigned)(pshift * cs);
+        const unsigned bias = 2u * (unsigned)(pshift * st.cs);
         const unsigned sbytes = use1 ? bytes1 : bytes0;
-        const __amdgpu_buffer_rsrc_t ra = make_rsrc(sb + sterm - bias, sbytes + bias - sterm);
-        const __amdgpu_buffer_rsrc_t rb = make_rsrc(u_wt + 2 * k0, wbytes - 2 * k0);
-        const int lim = p.cin - cbase;
-#pragma unroll
-        for (int i = 0; i < SA; ++i) {
+        st.ra = make_rsrc(sb + sterm - bias, sbytes + bias - sterm);
+        st.rb = make_rsrc(u_wt + 2 * k0, wbytes - 2 * k0);
+        st.lim = p.cin - cbase;
+        return st;
+    }
+    // DMA piece i (< PMAX; A slots first) of this wave into the stage image at lds;
+    // i is a constant after unrolling, so the slot arrays stay in registers
+    __device__ __forceinline__ void piece(const Stage& st, char* lds, int wave, int i) const {
+        if (i < SA) {
             const int ch = chunk_of(row_of(wave, i));
             // branch-free: a dropped tap / channel tail pushes the offset past num_records
             unsigned ok = (a_mask[i] >> tap) & 1u;
-            if (ctail) ok &= (unsigned)(ch < lim);
-            const unsigned off = (unsigned)(2 * (a_pix[i] * cs + ch)) | ((ok - 1u) & kOOB);
-            dma_piece(ra, lds + (wave + i * NW) * 1024, off);
+            if (ctail) ok &= (unsigned)(ch < st.lim);
+            const unsigned off = (unsigned)(2 * (a_pix[i] * st.cs + ch)) | ((ok - 1u) & kOOB);
+            dma_piece(st.ra, lds + (wave + i * NW) * 1024, off);
+        } else {
+            const int j = i - SA;
+            if (j == SB - 1 && (NB % NW) != 0 && wave >= (NB % NW)) return;   // wave-uniform
+            dma_piece(st.rb, lds + BM * RB + (wave + j * NW) * 1024, b_off[j]);
         }
-#pragma unroll
-        for (int i = 0; i < SB; ++i) {
-            if (i == SB - 1 && (NB % NW) != 0 && wave >= (NB % NW)) break;   // wave-uniform
-            dma_piece(rb, lds + BM * RB + (wave + i * NW) * 1024, b_off[i]);
-        }
-        if (KS == 3 && p.cmajor) {                        // taps inner (C2D_GEMM_KORDER)
+    }
+    __device__ __forceinline__ void advance() {
+        if (KS == 3 && cbase_major) {                     // taps inner (C2D_GEMM_KORDER)
             if (++tap == 9) { tap = 0; cbase += BK; }
         } else {
             cbase += BK;
-            if (KS == 3 && cbase >= p.cin) { cbase = 0; ++tap; }
+            if (KS == 3 && cbase >= cin_) { cbase = 0; ++tap; }
         }
+    }
+
+    // stage the next K step into [A rows | B rows] at lds in one burst
+    __device__ __forceinline__ void issue(const IgemmParams& p, int kt, char* lds, int wave) {
+        (void)kt;
+        const Stage st = prep(p);
+#pragma unroll
+        for (int i = 0; i < PMAX; ++i) piece(st, lds, wave, i);
+        advance();
     }
 };
 
@@ -201,7 +221,13 @@ __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x1
 // wave waits until all but its own younger stages landed (counted vmcnt) and the
 // workgroup passes a raw s_barrier (no vmcnt(0) drain), then re-issues into the
 // slot freed by step kt-1.
-template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, bool DB>
+//
+// MODE 0: the next stage's DMA pieces issue in one burst after the barrier.
+// MODE 1: as 0 with double-buffered fragment registers.
+// MODE 2: the pieces are dealt between the MFMAs of the step (one after every
+//   ~NSLOT / PMAX MFMAs), so their issue cost (60-185 cycles each) overlaps the
+//   32-cycle MFMAs instead of stalling both waves of the SIMD together.
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB>
 __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) {
     constexpr int NW = WM * WN;
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -251,9 +277,38 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (kt + STAGES - 1 < ke && !(p.abl & 1)) ld.issue(p, kt + STAGES - 1, smem + wr * STAGE, wave);
+        const bool do_issue = kt + STAGES - 1 < ke && !(p.abl & 1);
+        if (DB != 2 && do_issue) ld.issue(p, kt + STAGES - 1, smem + wr * STAGE, wave);
         const char* S = smem + rd * STAGE;
-        if (p.abl & 2) {   // timing ablation: fragments read and kept live, no MFMA
+        if (DB == 2 && !(p.abl & 2)) {
+            constexpr int NSLOT = NS * TM * TN, P = Loader::PMAX;
+            // with one stage in flight the pieces must land within this step: keep
+            // them in its first two thirds
+            constexpr int SPAN = STAGES > 2 ? NSLOT : (2 * NSLOT) / 3;
+            typename Loader::Stage st = ld.prep(p);
+            char* W = smem + wr * STAGE;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                f16x8 fa[TM], fb[TN];
+#pragma unroll
+                for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s]);
+#pragma unroll
+                for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s]);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+#pragma unroll
+                    for (int a = 0; a < TN; ++a) {
+                        const int slot = (s * TM + b) * TN + a;
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+                        for (int q = 0; q < P; ++q)
+                            if (slot == (q * SPAN) / P && do_issue) ld.piece(st, W, wave, q);   // wave-uniform
+                    }
+                __builtin_amdgcn_s_setprio(0);
+            }
+            if (do_issue) ld.advance();
+        } else if (p.abl & 2) {   // timing ablation: fragments read and kept live, no MFMA
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
 #pragma unroll
@@ -263,7 +318,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
                 for (int t = 0; t < TM; ++t)
                     asm volatile("" :: "v"(*reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s])));
             }
-        } else if (DB) {
+        } else if (DB == 1) {
             f16x8 fa[2][TM], fb[2][TN];
 #pragma unroll
             for (int t = 0; t < TN; ++t) fb[0][t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[0]);
@@ -329,7 +384,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
     epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, bool DB>
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB>
 static void launch_m32(const IgemmParams& p, hipStream_t s) {
     constexpr int smem = STAGES * (WM * TM + WN * TN) * 32 * 2 * BK;
     static_assert(smem <= 160 * 1024, "LDS ring too large");
@@ -347,7 +402,7 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
     }
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int ST, bool DB>
+template <int WM, int WN, int TM, int TN, int BK, int ST, int DB>
 static void run_m32(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     p.gx = (cout + BN - 1) / BN;
