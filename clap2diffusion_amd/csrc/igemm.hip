@@ -727,6 +727,8 @@ static const DmaTile kDmaTiles[] = {
     {21, 256, 320, 1, 0.0f, true},
     {24, 256, 320, 1, 0.0f, true},
     {26, 128, 320, 1, 0.0f, true},
+    {25, 256, 320, 1, 0.0f, true},
+    {22, 256, 320, 1, 0.0f, true},
     {30, 256, 320, 1, 0.0f, true},
     {7, 128, 320, 1, 3.1f, false},
     {1, 256, 128, 1, 2.9f, true},
@@ -760,7 +762,8 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
     return best;
 }
 
-// C2D_GEMM_ABL: timing ablation of the DMA kernel (1 = no DMA, 2 = no MFMA); wrong results by design
+// C2D_GEMM_ABL: timing ablation of the DMA kernels (1 = no DMA, 2 = no MFMA; m32: 4 = no epilogue,
+// 8 = with 2, no fragment reads either); wrong results by design
 static int gemm_abl() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_GEMM_ABL"); v = e ? atoi(e) : 0; }
@@ -810,9 +813,9 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     // tile once it (nearly) fills the chip, and with split-K for the long-K convs
     // (9 * cin >= 5760: L1 / L2 resnet and up-block convs); 128x320 below that
     const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
-    if (t24 >= 192) return {24, 1, nk};
+    if (t24 >= 192) return {25, 1, nk};
     if (nk >= 90 && t24 >= 64) {
-        DmaPlan pl = plan_dma(M, cout, nk, geglu, 24, 0);
+        DmaPlan pl = plan_dma(M, cout, nk, geglu, 25, 0);
         if (pl.id) return pl;
     }
     const long t7 = geglu ? ((M + 255) / 256) * ((cout + 127) / 128) : ((M + 127) / 128) * ((cout + 319) / 320);
@@ -828,6 +831,8 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 64
         case 21: return run_m32<4, 2, 2, 5, 32, 4, 2>(p, ksize, cout, s);      // as 20, DMA interleaved with MFMAs
         case 24: return run_m32<4, 2, 2, 5, 64, 2, 2>(p, ksize, cout, s);      // as 23, DMA interleaved with MFMAs
+        case 25: return run_m32<4, 2, 2, 5, 64, 2, 3>(p, ksize, cout, s);      // as 24, fragments double-buffered
+        case 22: return run_m32<4, 2, 2, 5, 32, 4, 3>(p, ksize, cout, s);      // as 21, fragments double-buffered
         case 26: return run_m32<4, 2, 1, 5, 32, 5, 2>(p, ksize, cout, s);      // 128x320, 8 waves of 32x160, BK 32
         case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80

@@ -227,8 +227,12 @@ __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x1
 // MODE 2: the pieces are dealt between the MFMAs of the step (one after every
 //   ~NSLOT / PMAX MFMAs), so their issue cost (60-185 cycles each) overlaps the
 //   32-cycle MFMAs instead of stalling both waves of the SIMD together.
-template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB>
-__global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) {
+// MODE 3: as 2 with the fragments of sub-step s+1 read before the MFMAs of s.
+// WPE > 0: request WPE waves per SIMD (register cap 512 / WPE) so that several
+// smaller workgroups share a CU and one's epilogue overlaps another's main loop.
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE = 0>
+__global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
+igemm_m32_kernel(IgemmParams p) {
     constexpr int NW = WM * WN;
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int RB = 2 * BK, STAGE = (BM + BN) * RB, NS = BK / 16;
@@ -278,29 +282,39 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const bool do_issue = kt + STAGES - 1 < ke && !(p.abl & 1);
-        if (DB != 2 && do_issue) ld.issue(p, kt + STAGES - 1, smem + wr * STAGE, wave);
+        if (DB < 2 && do_issue) ld.issue(p, kt + STAGES - 1, smem + wr * STAGE, wave);
         const char* S = smem + rd * STAGE;
-        if (DB == 2 && !(p.abl & 2)) {
+        if (DB >= 2 && !(p.abl & 2)) {
             constexpr int NSLOT = NS * TM * TN, P = Loader::PMAX;
             // with one stage in flight the pieces must land within this step: keep
             // them in its first two thirds
             constexpr int SPAN = STAGES > 2 ? NSLOT : (2 * NSLOT) / 3;
+            constexpr int NB2 = DB == 3 ? 2 : 1;        // MODE 3: fragments double-buffered
             typename Loader::Stage st = ld.prep(p);
             char* W = smem + wr * STAGE;
+            f16x8 fa[NB2][TM], fb[NB2][TN];
+            auto load_frags = [&](int s, int bb) {
+#pragma unroll
+                for (int t = 0; t < TN; ++t) fb[bb][t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s]);
+#pragma unroll
+                for (int t = 0; t < TM; ++t) fa[bb][t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s]);
+            };
+            if (DB == 3) load_frags(0, 0);
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                f16x8 fa[TM], fb[TN];
-#pragma unroll
-                for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s]);
-#pragma unroll
-                for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo[s]);
+                const int cur = DB == 3 ? (s & 1) : 0;
+                if (DB == 3) {
+                    if (s + 1 < NS) load_frags(s + 1, cur ^ 1);
+                } else {
+                    load_frags(s, 0);
+                }
                 __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int b = 0; b < TM; ++b)
 #pragma unroll
                     for (int a = 0; a < TN; ++a) {
                         const int slot = (s * TM + b) * TN + a;
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[cur][a], fa[cur][b], acc[a][b], 0, 0, 0);
 #pragma unroll
                         for (int q = 0; q < P; ++q)
                             if (slot == (q * SPAN) / P && do_issue) ld.piece(st, W, wave, q);   // wave-uniform
@@ -310,7 +324,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
             if (do_issue) ld.advance();
         } else if (p.abl & 2) {   // timing ablation: fragments read and kept live, no MFMA
 #pragma unroll
-            for (int s = 0; s < NS; ++s) {
+            for (int s = 0; s < NS && !(p.abl & 8); ++s) {
 #pragma unroll
                 for (int t = 0; t < TN; ++t)
                     asm volatile("" :: "v"(*reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s])));
@@ -364,6 +378,15 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
         wr = (wr + 1 == STAGES) ? 0 : wr + 1;
     }
     const int mw0 = m0 + wm * TM * 32, nw0 = n0 + wn * TN * 32;
+    if (p.abl & 4) {   // timing ablation: no epilogue (the accumulators kept live)
+        float z = 0.f;
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+            for (int b = 0; b < TM; ++b) z += acc[a][b][0] + acc[a][b][15];
+        if (z == 12345.f) p.out[0] = (f16)z;   // never taken; keeps the MFMAs
+        return;
+    }
     if (p.ksplit > 1) {
         float* dst = p.ws + (size_t)slice * p.M * p.cout;
 #pragma unroll
@@ -384,11 +407,11 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_m32_kernel(IgemmParams p) 
     epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB>
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE>
 static void launch_m32(const IgemmParams& p, hipStream_t s) {
     constexpr int smem = STAGES * (WM * TM + WN * TN) * 32 * 2 * BK;
     static_assert(smem <= 160 * 1024, "LDS ring too large");
-    auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB>;
+    auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -402,14 +425,14 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
     }
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int ST, int DB>
+template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int WPE = 0>
 static void run_m32(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     p.gx = (cout + BN - 1) / BN;
     p.gy = (p.M + BM - 1) / BM;
     p.nkt *= 64 / BK;   // the planner counts 64-deep K steps
-    if (ksize == 1) launch_m32<WM, WN, TM, TN, BK, ST, 1, DB>(p, s);
-    else launch_m32<WM, WN, TM, TN, BK, ST, 3, DB>(p, s);
+    if (ksize == 1) launch_m32<WM, WN, TM, TN, BK, ST, 1, DB, WPE>(p, s);
+    else launch_m32<WM, WN, TM, TN, BK, ST, 3, DB, WPE>(p, s);
 }
 
 // ---------------------------------------------------------------------------

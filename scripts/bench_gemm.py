@@ -29,25 +29,30 @@ SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)
     ("L1 up conv 1920->640", 3, 32, 1920, 640),
     ("L3 conv 2560->1280", 3, 8, 2560, 1280),
     ("L2 qkv 1280->3840", 1, 16, 1280, 3840),
+    ("L0 GEGLU act 320->2x1280", 1, 64, 320, 2560, "geglu"),
+    ("L1 GEGLU act 640->2x2560", 1, 32, 640, 5120, "geglu"),
 ]
 
 
-def run(name, k, h, cin, cout, iters=20):
+def run(name, k, h, cin, cout, act=None, iters=20):
     x = torch.randn(N, h, h, cin, device=dev, dtype=torch.float16)
     w = torch.randn(cout, cin, k, k, device=dev) / math.sqrt(k * k * cin)
     wp, kp = ops.pack_conv_weight(w)
-    out = torch.empty(N, h, h, cout, device=dev, dtype=torch.float16)
+    out = torch.empty(N, h, h, cout // 2 if act == "geglu" else cout, device=dev, dtype=torch.float16)
     for _ in range(3):
-        ops.conv(x, wp, kp, cout, ksize=k, out=out)
+        ops.conv(x, wp, kp, cout, ksize=k, out=out, act=act)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
-        ops.conv(x, wp, kp, cout, ksize=k, out=out)
+        ops.conv(x, wp, kp, cout, ksize=k, out=out, act=act)
     e1.record()
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * N * h * h * cout * k * k * cin
     ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w, padding=k // 2).permute(0, 2, 3, 1)
+    if act == "geglu":   # packed [16 h | 16 g] column blocks (ops.geglu_interleave layout)
+        r = ref.reshape(*ref.shape[:-1], -1, 2, 16)
+        ref = (r[..., 0, :] * torch.nn.functional.gelu(r[..., 1, :])).reshape(*ref.shape[:-1], -1)
     err = ((out.float() - ref).norm() / ref.norm()).item()
     print(f"{name:26s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  relerr {err:.1e}", flush=True)
 
