@@ -39,7 +39,7 @@ struct IgemmParams {
     int nkt;     // K steps per slice
     float* ws;   // split-K fp32 partials [ksplit][M][cout]
     int abl;     // timing ablation bits (C2D_GEMM_ABL; 0 in production)
-    int lds_epi; // 32x32 kernels: LDS-staged coalesced epilogue (C2D_GEMM_LDSEPI, default on)
+    int lds_epi; // 32x32 kernels: 1 = LDS-staged epilogue (C2D_GEMM_LDSEPI or alignment), 0 = direct
     int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_GEMM_KORDER, default 1)
 };
 
@@ -781,10 +781,18 @@ static int gemm_korder() {
     return v;
 }
 
-static int gemm_lds_epi() {
+static int gemm_lds_epi() {   // C2D_GEMM_LDSEPI=1 forces the LDS-staged epilogue of the 32x32 kernels
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_GEMM_LDSEPI"); v = e ? atoi(e) : 1; }
     return v;
+}
+
+// the direct 32x32 epilogue stores 4-channel (8-B) runs and loads the bias as float4
+static bool epi_direct_ok(const c2d_conv_desc* d) {
+    const int out_cols = d->act == C2D_ACT_GEGLU ? d->cout / 2 : d->cout;
+    const uintptr_t a8 = (uintptr_t)d->out | (uintptr_t)d->resid | (uintptr_t)d->temb;
+    return (out_cols % 4) == 0 && (d->out_ld % 4) == 0 && (!d->resid || (d->resid_ld % 4) == 0) &&
+           (!d->temb || (d->temb_ld % 4) == 0) && (a8 & 7) == 0 && ((uintptr_t)d->bias & 15) == 0;
 }
 
 // C2D_GEMM_SPLIT=s forces s K slices (when the workspace allows); 0 = model
@@ -831,7 +839,7 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 64
         case 21: return run_m32<4, 2, 2, 5, 32, 4, 2>(p, ksize, cout, s);      // as 20, DMA interleaved with MFMAs
         case 24: return run_m32<4, 2, 2, 5, 64, 2, 2>(p, ksize, cout, s);      // as 23, DMA interleaved with MFMAs
-        case 25: return run_m32<4, 2, 2, 5, 64, 2, 3>(p, ksize, cout, s);      // as 24, fragments double-buffered
+        case 25: return run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s);   // as 24, fragments double-buffered
         case 22: return run_m32<4, 2, 2, 5, 32, 4, 3>(p, ksize, cout, s);      // as 21, fragments double-buffered
         case 26: return run_m32<4, 2, 1, 5, 32, 5, 2>(p, ksize, cout, s);      // 128x320, 8 waves of 32x160, BK 32
         case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
@@ -912,7 +920,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.nkt = d->kpad / 64;
     p.ws = nullptr;
     p.abl = gemm_abl();
-    p.lds_epi = gemm_lds_epi();
+    p.lds_epi = (gemm_lds_epi() || !epi_direct_ok(d)) ? 1 : 0;
     p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {

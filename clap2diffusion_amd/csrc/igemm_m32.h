@@ -213,6 +213,70 @@ __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x1
     }
 }
 
+// Direct epilogue from the accumulators (no LDS round trip), the activation fixed
+// at compile time so the fully unrolled body stays small.  In the 32x32 D^T layout
+// lane l holds, for pixel m = lane & 31, the packed weight rows (r & 3) + 8 (r >> 2)
+// + 4 (l >> 5) of register r: four runs of 4 consecutive output channels -> 8-B
+// stores (lanes l and l + 32 complete 16 B of the row).  GEGLU packs [16 h | 16 g]
+// per 32 rows, so h (registers 0-7) and its gate (registers 8-15) share a lane.
+// Host contract (igemm.hip epi_direct_ok): output / residual / temb leading dims
+// and output width multiples of 4, those pointers 8-B and the bias 16-B aligned.
+template <int TM, int TN, int ACT>
+__device__ __forceinline__ void epilogue32_direct(const IgemmParams& p, const f32x16 (&acc)[TN][TM], int mw0,
+                                                  int nw0, int lane) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    constexpr bool GG = ACT == C2D_ACT_GEGLU;
+    const int lh = lane >> 5;
+    const int hw = p.oh * p.ow;
+    const int out_cols = GG ? (p.cout >> 1) : p.cout;
+#pragma unroll
+    for (int b = 0; b < TM; ++b) {
+        const int m = mw0 + b * 32 + (lane & 31);
+        if (m >= p.M) continue;
+        const f16* trow = p.temb ? p.temb + (size_t)(m / hw) * p.temb_ld : nullptr;
+        const f16* rrow = p.resid ? p.resid + (size_t)m * p.resid_ld : nullptr;
+        f16* orow = p.out + (size_t)m * p.out_ld;
+#pragma unroll
+        for (int a = 0; a < TN; ++a) {
+            const int jb = nw0 + a * 32;
+#pragma unroll
+            for (int g = 0; g < (GG ? 2 : 4); ++g) {
+                const int jp = jb + g * 8 + 4 * lh;                    // packed row of registers 4g..4g+3
+                const int j = GG ? (jb >> 1) + g * 8 + 4 * lh : jp;    // output column
+                if (j >= out_cols) continue;
+                float v[4] = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+                if (p.bias) {
+                    const float4 bb = *reinterpret_cast<const float4*>(p.bias + jp);
+                    v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+                }
+                if constexpr (GG) {
+                    float gt[4] = {acc[a][b][4 * g + 8], acc[a][b][4 * g + 9], acc[a][b][4 * g + 10], acc[a][b][4 * g + 11]};
+                    if (p.bias) {
+                        const float4 bb = *reinterpret_cast<const float4*>(p.bias + jp + 16);
+                        gt[0] += bb.x; gt[1] += bb.y; gt[2] += bb.z; gt[3] += bb.w;
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] *= gelu_f(gt[r]);
+                }
+                if (trow) {
+                    const h4 t = *reinterpret_cast<const h4*>(trow + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                if (rrow) {
+                    const h4 t = *reinterpret_cast<const h4*>(rrow + j);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += (float)t[r];
+                }
+                h4 o;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+                *reinterpret_cast<h4*>(orow + j) = o;
+            }
+        }
+    }
+}
+
 // WM x WN waves, each owning a (TM*32) x (TN*32) output tile (TM row tiles of
 // the activation side, TN column tiles of the weight side): D^T = W . A^T per
 // 32x32 tile.  Per 16-deep k sub-step a wave reads TM + TN fragments
@@ -230,7 +294,9 @@ __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x1
 // MODE 3: as 2 with the fragments of sub-step s+1 read before the MFMAs of s.
 // WPE > 0: request WPE waves per SIMD (register cap 512 / WPE) so that several
 // smaller workgroups share a CU and one's epilogue overlaps another's main loop.
-template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE = 0>
+// EACT >= 0: direct epilogue specialised for that activation (C2D_ACT_NONE / GEGLU);
+// -1: the LDS-staged epilogue with the activation read at run time.
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE = 0, int EACT = -1>
 __global__ void __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 igemm_m32_kernel(IgemmParams p) {
     constexpr int NW = WM * WN;
@@ -403,15 +469,19 @@ igemm_m32_kernel(IgemmParams p) {
         }
         return;
     }
+    if constexpr (EACT >= 0) {
+        epilogue32_direct<TM, TN, EACT>(p, acc, mw0, nw0, lane);
+        return;
+    }
     __syncthreads();
     epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE>
+template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE, int EACT>
 static void launch_m32(const IgemmParams& p, hipStream_t s) {
     constexpr int smem = STAGES * (WM * TM + WN * TN) * 32 * 2 * BK;
     static_assert(smem <= 160 * 1024, "LDS ring too large");
-    auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE>;
+    auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE, EACT>;
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -425,14 +495,26 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
     }
 }
 
-template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int WPE = 0>
+template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int KS, int WPE, bool DIRECT>
+static void launch_m32_act(const IgemmParams& p, hipStream_t s) {
+    if constexpr (DIRECT) {
+        if (!p.lds_epi && p.ksplit == 1 && p.act == C2D_ACT_NONE)
+            return launch_m32<WM, WN, TM, TN, BK, ST, KS, DB, WPE, C2D_ACT_NONE>(p, s);
+        if (!p.lds_epi && p.ksplit == 1 && p.act == C2D_ACT_GEGLU)
+            return launch_m32<WM, WN, TM, TN, BK, ST, KS, DB, WPE, C2D_ACT_GEGLU>(p, s);
+    }
+    launch_m32<WM, WN, TM, TN, BK, ST, KS, DB, WPE, -1>(p, s);
+}
+
+// DIRECT: also instantiate the direct-epilogue kernels (used when p.lds_epi == 0)
+template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int WPE = 0, bool DIRECT = false>
 static void run_m32(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     p.gx = (cout + BN - 1) / BN;
     p.gy = (p.M + BM - 1) / BM;
     p.nkt *= 64 / BK;   // the planner counts 64-deep K steps
-    if (ksize == 1) launch_m32<WM, WN, TM, TN, BK, ST, 1, DB, WPE>(p, s);
-    else launch_m32<WM, WN, TM, TN, BK, ST, 3, DB, WPE>(p, s);
+    if (ksize == 1) launch_m32_act<WM, WN, TM, TN, BK, ST, DB, 1, WPE, DIRECT>(p, s);
+    else launch_m32_act<WM, WN, TM, TN, BK, ST, DB, 3, WPE, DIRECT>(p, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -49,7 +49,8 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
                 shift[q][i] = gn_read(s0, s1, c0, c1, img, (c / cpg) * cpg);
             }
         }
-        for (int pix = p_begin + r0; pix < p_end; pix += R) {
+#pragma unroll 4
+        for (int pix = p_begin + r0; pix < p_end; pix += R) {   // 4 loads in flight per thread
             const size_t gp = img + pix;
 #pragma unroll
             for (int q = 0; q < CPT; ++q) {
@@ -192,6 +193,94 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s
             o[j] = (f16)y;
         }
         *reinterpret_cast<f16x8*>(out + pix * cin + c) = o;
+    }
+}
+
+// Single-launch GroupNorm (+ SiLU) for small images: one workgroup owns image n
+// and a chunk of CB channels (whole groups, CB % 8 == 0); L = CB / 8 lanes per
+// pixel row, R = 256 / L rows.  Pass 1 accumulates per-thread shifted moments
+// (fp32), the block folds them in a fixed order (fp64) -> per-group mean / rstd
+// -> per-channel affine in LDS; pass 2 re-reads the slab (L2 / MALL resident)
+// and writes act(x * scale + shift).  Deterministic; replaces partial + finalize
+// + apply (three launches of a few microseconds each) where the image is small.
+__global__ void __launch_bounds__(256) gn_fused_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
+                                                       int c1, int hw, int cpg, int cb, float eps,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       int silu, f16* __restrict__ out) {
+    __shared__ float red[2 * 2048];            // [R][CB][2], R * CB = 256 * 8
+    __shared__ double gsum[256], gsq[256];     // per channel of the chunk (CB <= 256)
+    __shared__ float aff[2 * 256];             // scale | shift per channel of the chunk
+    const int cin = c0 + c1;
+    const int L = cb >> 3, R = 256 / L;
+    const int n = blockIdx.y, cbase = blockIdx.x * cb;
+    const int t = threadIdx.x, lane_c = t % L, r0 = t / L;
+    const bool active = r0 < R && cbase + lane_c * 8 < cin;
+    const int c = cbase + lane_c * 8;
+    const size_t img = (size_t)n * hw;
+    const f16* src = (c < c0) ? (s0 + c) : (s1 + (c - c0));
+    const int ld = (c < c0) ? c0 : c1;
+    float sh[8], sum[8], sq[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sum[i] = 0.f; sq[i] = 0.f; sh[i] = 0.f; }
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sh[i] = gn_read(s0, s1, c0, c1, img, ((c + i) / cpg) * cpg);
+#pragma unroll 4
+        for (int pix = r0; pix < hw; pix += R) {
+            const f16x8 v = *reinterpret_cast<const f16x8*>(src + (img + pix) * ld);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float d = (float)v[i] - sh[i];
+                sum[i] += d;
+                sq[i] += d * d;
+            }
+        }
+    }
+    if (r0 < R) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            red[(r0 * cb + lane_c * 8 + i) * 2] = sum[i];
+            red[(r0 * cb + lane_c * 8 + i) * 2 + 1] = sq[i];
+        }
+    }
+    __syncthreads();
+    if (t < cb) {
+        double a = 0.0, b = 0.0;
+        for (int r = 0; r < R; ++r) { a += (double)red[(r * cb + t) * 2]; b += (double)red[(r * cb + t) * 2 + 1]; }
+        gsum[t] = a;
+        gsq[t] = b;
+    }
+    __syncthreads();
+    if (t < cb && cbase + t < cin) {
+        const int gl = t / cpg;                  // group within the chunk (chunks hold whole groups)
+        double a = 0.0, b = 0.0;
+        for (int i = 0; i < cpg; ++i) { a += gsum[gl * cpg + i]; b += gsq[gl * cpg + i]; }
+        const double cnt = (double)hw * cpg;
+        const double m1 = a / cnt;
+        double var = b / cnt - m1 * m1;
+        if (var < 0.0) var = 0.0;
+        const float mean = (float)(gn_read(s0, s1, c0, c1, img, cbase + gl * cpg) + m1);
+        const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+        const float scl = gamma[cbase + t] * rstd;
+        aff[t] = scl;
+        aff[256 + t] = beta[cbase + t] - mean * scl;
+    }
+    __syncthreads();
+    if (!active) return;
+    float av[8], bv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { av[i] = aff[lane_c * 8 + i]; bv[i] = aff[256 + lane_c * 8 + i]; }
+#pragma unroll 4
+    for (int pix = r0; pix < hw; pix += R) {
+        const f16x8 v = *reinterpret_cast<const f16x8*>(src + (img + pix) * ld);
+        f16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float y = fmaf((float)v[i], av[i], bv[i]);
+            if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+            o[i] = (f16)y;
+        }
+        *reinterpret_cast<f16x8*>(out + (img + pix) * cin + c) = o;
     }
 }
 
@@ -351,4 +440,61 @@ extern "C" int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, i
     hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
                        (const f16*)src1, c0, c1, hw, nchunks, scale, shift, silu, (f16*)out);
     return check_launch();
+}
+
+// channels per fused-GN workgroup: whole groups, a multiple of 8, <= 256, as few as
+// keep the launch at >= 256 workgroups; 0 when the shape does not fit the kernel
+static int gn_fused_cb(int n, int cin, int groups) {
+    const int cpg = cin / groups;
+    int u = cpg;
+    while (u % 8) u += cpg;                       // lcm(cpg, 8)
+    if (u > 256) return 0;
+    int cb = u;
+    while (cb * 2 <= 256 && cin % (cb * 2) == 0 && (long)n * (cin / (cb * 2)) >= 256) cb *= 2;
+    return cb;
+}
+
+// pixels per image up to which the single-launch kernel is used (C2D_GN_FUSED_HW).
+// Graph-replayed per call at N = 16 (scripts/bench_norm_graph.py): 8^2 x 1280
+// 16.8 -> 6.2 us, 16^2 x 1280 21.3 -> 13.0 us, but 32^2 x 640 23.1 -> 26.6 us
+// (40-channel chunks read 80-B row pieces over 1024 pixels) and 64^2 2-5x slower.
+static int gn_fused_max_hw() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GN_FUSED_HW"); v = e ? atoi(e) : 256; }
+    return v;
+}
+
+static bool gn_use_fused(int n, int cin, int hw, int groups) {
+    return gn_fused_cb(n, cin, groups) > 0 && hw <= gn_fused_max_hw();
+}
+
+extern "C" size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups) {
+    if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return 0;
+    if (gn_use_fused(n, c, hw, groups)) return 0;
+    return c2d_groupnorm_workspace_size(n, c, hw) + (size_t)n * c * 2 * sizeof(float);
+}
+
+extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups, float eps,
+                             const float* gamma, const float* beta, int silu, void* out, void* ws, size_t ws_bytes,
+                             void* stream) {
+    if (!src0 || !gamma || !beta || !out) return C2D_E_ARG;
+    if (c1 > 0 && !src1) return C2D_E_ARG;
+    const int cin = c0 + c1;
+    if ((c0 & 7) || (c1 & 7) || cin <= 0 || groups <= 0 || cin % groups) return C2D_E_SHAPE;
+    if (cin / groups > 256 || n <= 0 || hw <= 0) return C2D_E_SHAPE;
+    if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out)) return C2D_E_ALIGN;
+    hipStream_t s = (hipStream_t)stream;
+    if (gn_use_fused(n, cin, hw, groups)) {
+        const int cb = gn_fused_cb(n, cin, groups);
+        hipLaunchKernelGGL(gn_fused_kernel, dim3((cin + cb - 1) / cb, n), dim3(256), 0, s, (const f16*)src0,
+                           (const f16*)src1, c0, c1, hw, cin / groups, cb, eps, gamma, beta, silu, (f16*)out);
+        return check_launch();
+    }
+    if (!ws || ws_bytes < c2d_groupnorm_run_workspace_size(n, cin, hw, groups) || !aligned16(ws)) return C2D_E_ARG;
+    const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
+    float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
+    float* shift = scale + (size_t)n * cin;
+    int rc = c2d_groupnorm_stats(src0, src1, c0, c1, n, hw, groups, eps, gamma, beta, scale, shift, ws, stream);
+    if (rc != C2D_OK) return rc;
+    return c2d_groupnorm_apply(src0, src1, c0, c1, n, hw, scale, shift, silu, out, stream);
 }

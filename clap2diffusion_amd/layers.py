@@ -81,8 +81,8 @@ class HGroupNorm(nn.Module):
         return ops.group_norm_stats(x, self.num_groups, self.eps, self.weight, self.bias, x2=x2)
 
     def apply(self, x: torch.Tensor, x2: torch.Tensor | None = None, silu: bool = False) -> torch.Tensor:
-        """act(GroupNorm(cat[x, x2])) materialised once (stats + apply kernels)."""
-        return ops.group_norm_apply(x, self.stats(x, x2), silu, x2=x2)
+        """act(GroupNorm(cat[x, x2])) materialised once (c2d_groupnorm)."""
+        return ops.group_norm(x, self.num_groups, self.eps, self.weight, self.bias, silu, x2=x2)
 
 
 class HLayerNorm(nn.Module):

@@ -154,6 +154,25 @@ def group_norm_apply(x: torch.Tensor, gn, silu: bool, x2: torch.Tensor | None = 
     return out
 
 
+def group_norm(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor, silu: bool,
+               x2: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """act(GroupNorm(cat[x, x2])) in one c2d_groupnorm call (single fused kernel for
+    small images, stats + apply otherwise)."""
+    _require(x, "x")
+    n, c0 = x.shape[0], x.shape[-1]
+    c1 = x2.shape[-1] if x2 is not None else 0
+    hw = x.numel() // (n * c0)
+    c = c0 + c1
+    if out is None:
+        out = torch.empty((*x.shape[:-1], c), device=x.device, dtype=F16)
+    wsb = lib().c2d_groupnorm_run_workspace_size(n, c, hw, groups)
+    ws = torch.empty((wsb + 15) // 16 * 4, device=x.device, dtype=torch.float32) if wsb else None
+    rc = lib().c2d_groupnorm(ptr(x), ptr(x2), c0, c1, n, hw, groups, eps, ptr(gamma), ptr(beta), int(silu),
+                             ptr(out), ptr(ws), wsb, stream_ptr())
+    check(rc, "c2d_groupnorm")
+    return out
+
+
 def layer_norm_stats(x2d: torch.Tensor, eps: float) -> torch.Tensor:
     _require(x2d, "x")
     m, c = x2d.shape

@@ -131,6 +131,22 @@ int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, int c1, int 
                         const float* scale, const float* shift, int silu, void* out, void* stream);
 
 /*
+ * act(GroupNorm(cat[src0, src1])) in one call -- what HGroupNorm.apply (the
+ * ResnetBlock2D.norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out and VAE
+ * norms) needs.  Small images (hw <= 256 pixels) run a single kernel: one
+ * workgroup per (image, chunk of whole groups) computes the statistics, folds them in
+ * a fixed order and applies in a second pass over the L2 / MALL-resident slab.
+ * Larger ones run c2d_groupnorm_stats + c2d_groupnorm_apply with their partials and
+ * tables carved from ws (>= c2d_groupnorm_run_workspace_size(n, c0+c1, hw, groups)
+ * bytes, 16-B aligned; the size is 0 -- ws may be NULL -- when the single kernel
+ * runs).  Deterministic either way.
+ */
+size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups);
+int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups,
+                  float eps, const float* gamma, const float* beta, int silu, void* out,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/*
  * LayerNorm over rows of a row-major fp16 [m][c] matrix (leading dim ld).
  * c2d_layernorm_stats writes (mean, rstd) [m][2] for the C2D_PRO_LN prologue;
  * c2d_layernorm writes the normalised fp16 rows (out_ld) with gamma/beta.

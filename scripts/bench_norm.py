@@ -37,9 +37,10 @@ for h, c0, c1 in SHAPES:
     gn = st()
     out = torch.empty(N, h, h, c, device=dev, dtype=torch.float16)
     t_ap = timed(lambda: ops.group_norm_apply(x, gn, True, x2=x2, out=out))
+    t_one = timed(lambda: ops.group_norm(x, 32, 1e-5, g, b, True, x2=x2, out=out))
     xc = torch.cat([x, x2], -1) if x2 is not None else x
     ref = F.silu(F.group_norm(xc.permute(0, 3, 1, 2).float(), 32, g, b, 1e-5)).permute(0, 2, 3, 1)
     err = ((out.float() - ref).norm() / ref.norm()).item()
     mb = N * h * h * c * 2 / 1e6
     print(f"GN {h:3d}^2 c={c0}+{c1}: stats {t_st:7.1f} us ({mb / t_st:6.0f} GB/s)  apply {t_ap:7.1f} us "
-          f"({2 * mb / t_ap:6.0f} GB/s)  relerr {err:.1e}", flush=True)
+          f"({2 * mb / t_ap:6.0f} GB/s)  one-call {t_one:7.1f} us  relerr {err:.1e}", flush=True)

@@ -358,3 +358,33 @@ def test_groupnorm_deterministic(dev):
     g, b = torch.ones(320, device=dev), torch.zeros(320, device=dev)
     r = [ops.group_norm_stats(x, 32, 1e-5, g, b)[0] for _ in range(3)]
     assert all(torch.equal(r[0], t) for t in r[1:])
+
+
+# c2d_groupnorm: the single-kernel path (hw <= 256) and the stats + apply
+# pipeline, one- and two-source inputs, the UNet's channel / group shapes
+@pytest.mark.parametrize("n,h,c0,c1,groups,silu,eps", [
+    (2, 8, 1280, 0, 32, True, 1e-5),       # level-3 resnet norm (cpg 40)
+    (2, 8, 1280, 1280, 32, True, 1e-5),    # level-3 up-block concat (cpg 80)
+    (2, 16, 640, 320, 32, False, 1e-6),    # concat seam inside a group (cpg 30)
+    (4, 16, 320, 0, 32, True, 1e-5),       # cpg 10
+    (3, 16, 128, 0, 32, True, 1e-6),       # VAE-style cpg 4
+    (2, 32, 640, 0, 32, True, 1e-5),       # 32^2: stats + apply pipeline
+    (16, 64, 320, 0, 32, True, 1e-5),      # level-0 shape: stats + apply pipeline
+])
+def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
+    x0 = gen(n, c0, h, h, seed=60) + 0.5
+    x1 = gen(n, c1, h, h, seed=61) * 2 if c1 else None
+    xc = torch.cat([x0, x1], 1) if c1 else x0
+    c = c0 + c1
+    gamma, beta = gen(c, seed=62) * 0.1 + 1, gen(c, seed=63) * 0.1
+    a = nhwc(x0).half().to(dev)
+    b = nhwc(x1).half().to(dev) if c1 else None
+    # reference on the fp16-rounded input
+    ref = F.group_norm(torch.cat([nchw(a.float().cpu())] + ([nchw(b.float().cpu())] if c1 else []), 1),
+                       groups, gamma, beta, eps)
+    if silu:
+        ref = F.silu(ref)
+    out = ops.group_norm(a, groups, eps, gamma.float().to(dev), beta.float().to(dev), silu, x2=b)
+    close(nchw(out), ref, tol_max=5e-3, tol_l2=1e-3)
+    again = ops.group_norm(a, groups, eps, gamma.float().to(dev), beta.float().to(dev), silu, x2=b)
+    assert torch.equal(out, again)
