@@ -497,9 +497,11 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
 
 template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int KS, int WPE, bool DIRECT>
 static void launch_m32_act(const IgemmParams& p, hipStream_t s) {
+    // direct only for GEGLU (and only with C2D_GEMM_LDSEPI=0): plain outputs are
+    // faster through the LDS image (its 16-B coalesced stores beat the 8-B row
+    // pieces: L0 qkv 69.5 vs 78.8 us); GEGLU alone is faster direct (L0 320 -> 2 x
+    // 1280: 170 vs 190 us) but not inside the full step
     if constexpr (DIRECT) {
-        if (!p.lds_epi && p.ksplit == 1 && p.act == C2D_ACT_NONE)
-            return launch_m32<WM, WN, TM, TN, BK, ST, KS, DB, WPE, C2D_ACT_NONE>(p, s);
         if (!p.lds_epi && p.ksplit == 1 && p.act == C2D_ACT_GEGLU)
             return launch_m32<WM, WN, TM, TN, BK, ST, KS, DB, WPE, C2D_ACT_GEGLU>(p, s);
     }

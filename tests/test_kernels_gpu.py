@@ -245,6 +245,50 @@ def test_geglu(dev):
     close(out, ref)
 
 
+# shapes large enough for the planner's 256x320 tile (>= 192 output tiles), its
+# epilogue variants (scripts/gpu_epi_ab.sh runs these with C2D_GEMM_LDSEPI=0 and 1);
+# torch fp32 on the device is the reference
+def test_m32_direct_epilogue_geglu(dev):
+    m, c = 16384, 320
+    inner = 4 * c
+    x = gen(m, c, seed=70).to(dev)
+    w = gen(2 * inner, c, seed=71, scale=1 / math.sqrt(c)).to(dev)
+    b = (gen(2 * inner, seed=72) * 0.1).to(dev)
+    r = gen(m, inner, seed=73).to(dev)
+    xh, rh = x.half(), r.half()
+    hh, gg = F.linear(xh.float(), w, b).chunk(2, dim=-1)
+    ref = hh * F.gelu(gg) + rh.float()
+    wi, bi = ops.geglu_interleave(w, b)
+    wp, kp = ops.pack_linear_weight(wi)
+    out = ops.conv(xh, wp, kp, 2 * inner, ksize=1, bias=bi.float(), act="geglu", resid=rh)
+    close(out, ref)
+
+
+def test_m32_direct_epilogue_conv_temb_resid(dev):
+    n, h, cin, cout = 12, 64, 320, 320
+    x = gen(n, cin, h, h, seed=74).to(dev)
+    w = gen(cout, cin, 3, 3, seed=75, scale=1 / math.sqrt(9 * cin)).to(dev)
+    b = (gen(cout, seed=76) * 0.1).to(dev)
+    temb = gen(n, cout, seed=77).to(dev)
+    resid = gen(n, cout, h, h, seed=78).to(dev)
+    xh, th, rh = x.half(), temb.half(), resid.half()
+    ref = F.conv2d(xh.float(), w, b, padding=1) + th.float()[:, :, None, None] + rh.float()
+    wp, kp = ops.pack_conv_weight(w)
+    out = ops.conv(nhwc(xh), wp, kp, cout, ksize=3, bias=b.float(), temb=th, resid=nhwc(rh))
+    close(nchw(out), ref)
+
+
+def test_m32_direct_epilogue_linear_bias(dev):
+    m, cin, cout = 16384, 320, 960
+    x = gen(m, cin, seed=79).to(dev)
+    w = gen(cout, cin, seed=80, scale=1 / math.sqrt(cin)).to(dev)
+    b = (gen(cout, seed=81) * 0.1).to(dev)
+    ref = F.linear(x.half().float(), w, b)
+    wp, kp = ops.pack_linear_weight(w)
+    out = ops.conv(x.half(), wp, kp, cout, ksize=1, bias=b.float())
+    close(out, ref)
+
+
 def test_silu_prologue(dev):
     x = gen(16, 1280, seed=36)
     w = gen(2560, 1280, seed=37, scale=1 / math.sqrt(1280))
