@@ -728,6 +728,8 @@ static const DmaTile kDmaTiles[] = {
     {24, 256, 320, 1, 0.0f, true},
     {26, 128, 320, 1, 0.0f, true},
     {25, 256, 320, 1, 0.0f, true},
+    {28, 256, 256, 1, 0.0f, true},
+    {29, 256, 128, 1, 0.0f, true},
     {22, 256, 320, 1, 0.0f, true},
     {30, 256, 320, 1, 0.0f, true},
     {7, 128, 320, 1, 3.1f, false},
@@ -823,6 +825,14 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     // rules from the shape sweeps (scripts/sweep_tiles.sh): the 256x320 interleaved-DMA
     // tile once it (nearly) fills the chip, and with split-K for the long-K convs
     // (9 * cin >= 5760: L1 / L2 resnet and up-block convs); 128x320 below that
+    // VAE widths (128 / 256 / 512 channels) leave 320-wide tiles 20-60 % empty: the
+    // 256x256 / 256x128 variants of the same kernel (512^2 x 128 ch conv: 250 vs 402 us;
+    // 256 / 512 ch: 11-14 % faster)
+    if (!geglu && cout % 320 != 0) {
+        const long mt = (M + 255) / 256;
+        if (cout % 256 == 0 && mt * (cout / 256) >= 192) return {28, 1, nk};
+        if (cout % 256 != 0 && cout % 128 == 0 && mt * (cout / 128) >= 192) return {29, 1, nk};
+    }
     const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
     if (t24 >= 192) return {25, 1, nk};
     if (nk >= 90 && t24 >= 64) {
@@ -844,6 +854,8 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 24: return run_m32<4, 2, 2, 5, 64, 2, 2>(p, ksize, cout, s);      // as 23, DMA interleaved with MFMAs
         case 25: return run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s);   // as 24, fragments double-buffered
         case 22: return run_m32<4, 2, 2, 5, 32, 4, 3>(p, ksize, cout, s);      // as 21, fragments double-buffered
+        case 28: return run_m32<4, 2, 2, 4, 64, 2, 3>(p, ksize, cout, s);      // 256x256, 8 waves of 64x128
+        case 29: return run_m32<4, 2, 2, 2, 64, 3, 3>(p, ksize, cout, s);      // 256x128, 8 waves of 64x64, 3 stages
         case 26: return run_m32<4, 2, 1, 5, 32, 5, 2>(p, ksize, cout, s);      // 128x320, 8 waves of 32x160, BK 32
         case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80

@@ -29,16 +29,24 @@ SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)
     ("L1 up conv 1920->640", 3, 32, 1920, 640),
     ("L3 conv 2560->1280", 3, 8, 2560, 1280),
     ("L2 qkv 1280->3840", 1, 16, 1280, 3840),
+    ("L1 proj 640->640", 1, 32, 640, 640),
+    ("L2 proj 1280->1280", 1, 16, 1280, 1280),
+    ("L2 ff2 5120->1280", 1, 16, 5120, 1280),
     ("L0 GEGLU act 320->2x1280", 1, 64, 320, 2560, "geglu"),
+    ("VAE 512^2 conv 128->128 n2", 3, 512, 128, 128, None, 2),
+    ("VAE 256^2 conv 256->256 n2", 3, 256, 256, 256, None, 2),
+    ("VAE 512^2 conv 256->256 n2", 3, 512, 256, 256, None, 2),
+    ("VAE 128^2 conv 512->512 n2", 3, 128, 512, 512, None, 2),
+    ("VAE 64^2 conv 512->512 n8", 3, 64, 512, 512, None, 8),
     ("L1 GEGLU act 640->2x2560", 1, 32, 640, 5120, "geglu"),
 ]
 
 
-def run(name, k, h, cin, cout, act=None, iters=20):
-    x = torch.randn(N, h, h, cin, device=dev, dtype=torch.float16)
+def run(name, k, h, cin, cout, act=None, n=N, iters=20):
+    x = torch.randn(n, h, h, cin, device=dev, dtype=torch.float16)
     w = torch.randn(cout, cin, k, k, device=dev) / math.sqrt(k * k * cin)
     wp, kp = ops.pack_conv_weight(w)
-    out = torch.empty(N, h, h, cout // 2 if act == "geglu" else cout, device=dev, dtype=torch.float16)
+    out = torch.empty(n, h, h, cout // 2 if act == "geglu" else cout, device=dev, dtype=torch.float16)
     for _ in range(3):
         ops.conv(x, wp, kp, cout, ksize=k, out=out, act=act)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,7 +56,7 @@ def run(name, k, h, cin, cout, act=None, iters=20):
     e1.record()
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    fl = 2.0 * N * h * h * cout * k * k * cin
+    fl = 2.0 * n * h * h * cout * k * k * cin
     ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w, padding=k // 2).permute(0, 2, 3, 1)
     if act == "geglu":   # packed [16 h | 16 g] column blocks (ops.geglu_interleave layout)
         r = ref.reshape(*ref.shape[:-1], -1, 2, 16)

@@ -432,3 +432,22 @@ def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
     close(nchw(out), ref, tol_max=5e-3, tol_l2=1e-3)
     again = ops.group_norm(a, groups, eps, gamma.float().to(dev), beta.float().to(dev), silu, x2=b)
     assert torch.equal(out, again)
+
+
+# VAE widths: the planner's 256x128 (128 channels) and 256x256 (256 / 512 channels)
+# variants of the 32x32 tile; torch fp32 on the device is the reference
+@pytest.mark.parametrize("n,h,cin,cout", [
+    (2, 256, 128, 128),    # 256x128 tile, 3-stage ring
+    (2, 128, 256, 512),    # 256x256 tile
+    (1, 256, 512, 256),    # 256x256 tile, 18 K steps per 64 channels x 9 taps
+])
+def test_m32_vae_width_tiles(dev, n, h, cin, cout):
+    x = gen(n, cin, h, h, seed=90).to(dev)
+    w = gen(cout, cin, 3, 3, seed=91, scale=1 / math.sqrt(9 * cin)).to(dev)
+    b = (gen(cout, seed=92) * 0.1).to(dev)
+    r = gen(n, cout, h, h, seed=93).to(dev)
+    xh, rh = x.half(), r.half()
+    ref = F.conv2d(xh.float(), w, b, padding=1) + rh.float()
+    wp, kp = ops.pack_conv_weight(w)
+    out = ops.conv(nhwc(xh), wp, kp, cout, ksize=3, bias=b.float(), resid=nhwc(rh))
+    close(nchw(out), ref)
