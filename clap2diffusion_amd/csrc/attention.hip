@@ -54,7 +54,7 @@ template <int D, bool MASK>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
-                                                       int kv_div, int nqb) {
+                                                       int kv_div, int nqb, int abl) {
     using C = AttnCfg<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* Ks = smem;
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
     __syncthreads();
 
     for (int t = 0; t < ntiles; ++t) {
-        if (t + 1 < ntiles) gload(t + 1);
+        if (t + 1 < ntiles && !abl) gload(t + 1);
 
         // ---- S^T tiles: s[qg][kg] holds keys 16 kg + 4 g + r of query li
         f32x4 s[2][4], st[2][4];
@@ -266,7 +266,10 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
             }
         }
 
-        if (t + 1 < ntiles) {
+        // abl (C2D_ATTN_ABL=1): timing only, K/V tile 0 reused -- the restaging
+        // costs ~17 % of the d = 40 kernel; a two-slot LDS ring with one barrier per
+        // tile was measured slower (its address registers cost the third wave / SIMD)
+        if (t + 1 < ntiles && !abl) {
             __syncthreads();
             swrite();
             __syncthreads();
@@ -548,6 +551,12 @@ __global__ void __launch_bounds__(256) attn_pp_kernel(const f16* __restrict__ q,
 // in-flight S tile takes it to 148 VGPR + 24 AGPR = 2 waves/SIMD vs 126 + 40 = 3 for
 // attn_fwd_kernel<40>, and the doubled K/V ring halves the blocks LDS admits, so it is
 // off by default.
+static int attn_abl() {   // C2D_ATTN_ABL=1: timing ablation of the K/V staging (wrong results)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_ATTN_ABL"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
 static int attn_pipelined() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
@@ -577,10 +586,12 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
     }
     if (lk % 64 == 0)
         hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
-                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
+                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb,
+                           attn_abl());
     else
         hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
-                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb);
+                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb,
+                           attn_abl());
     return check_launch();
 }
 
