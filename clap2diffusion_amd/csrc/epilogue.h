@@ -13,23 +13,27 @@ namespace c2d {
 
 // W-column chunk body (W = 8: 16-B loads / stores; W = 4: 8-B, for outputs whose
 // width, leading dimensions or base addresses are only 4-element aligned, e.g. the
-// 4-channel conv_out).  img: fp32 [rows][pitchf] image of the block's rows m0..
-// and packed weight columns jp0 .. jp0 + cols (cols % 8 == 0; GEGLU: % 32 == 0).
-template <int W>
-__device__ __forceinline__ void epi_rows_w(const IgemmParams& p, const float* img, int pitchf, int rows, int cols,
-                                           int m0, int jp0, int lane) {
+// 4-channel conv_out).  img: fp32 [ROWS][pitchf] image of the block's rows m0..
+// and packed weight columns jp0 .. jp0 + COLS (COLS % 8 == 0; GEGLU: % 32 == 0).
+// The image geometry and the GEGLU flag are template parameters so the chunk ->
+// (row, column) split is constant-divisor arithmetic: with run-time divisors the
+// integer divisions cost as much VALU per chunk as the GELU itself.
+template <int W, bool GG, int ROWS, int COLS>
+__device__ __forceinline__ void epi_rows_t(const IgemmParams& p, const float* img, int pitchf, int m0, int jp0,
+                                           int lane) {
     typedef _Float16 hv __attribute__((ext_vector_type(W)));
-    const bool geglu = p.act == C2D_ACT_GEGLU;
-    const int cpr = geglu ? cols / (2 * W) : cols / W;      // W-wide output chunks per row
-    const int cpt = 16 / W;                                 // GEGLU: chunks per 32-row tile
+    constexpr int CPR = GG ? COLS / (2 * W) : COLS / W;   // W-wide output chunks per row
+    constexpr int CPT = 16 / W;                           // GEGLU: chunks per 32-row tile
+    static_assert(COLS % (GG ? 32 : 8) == 0, "epilogue image width");
     const int hw = p.oh * p.ow;
-    const int out_cols = geglu ? (p.cout >> 1) : p.cout;
-    for (int c = lane; c < rows * cpr; c += 64) {
-        const int row = c / cpr, cc = c - row * cpr;
+    const int out_cols = GG ? (p.cout >> 1) : p.cout;
+#pragma unroll 2
+    for (int c = lane; c < ROWS * CPR; c += 64) {
+        const int row = c / CPR, cc = c - row * CPR;
         const int m = m0 + row;
         int sc, jp, j;                                       // image column, packed row, output column
-        if (geglu) {
-            const int t = cc / cpt, q = cc - t * cpt;
+        if constexpr (GG) {
+            const int t = cc / CPT, q = cc - t * CPT;
             sc = t * 32 + q * W;
             jp = jp0 + sc;
             j = ((jp0 + t * 32) >> 1) + q * W;
@@ -53,7 +57,7 @@ __device__ __forceinline__ void epi_rows_w(const IgemmParams& p, const float* im
                 v[r] += bb.x; v[r + 1] += bb.y; v[r + 2] += bb.z; v[r + 3] += bb.w;
             }
         }
-        if (geglu) {
+        if constexpr (GG) {
             float g[W];
 #pragma unroll
             for (int r = 0; r < W; r += 4) {
@@ -93,14 +97,25 @@ __device__ __forceinline__ void epi_rows_w(const IgemmParams& p, const float* im
     }
 }
 
-__device__ __forceinline__ void epi_rows(const IgemmParams& p, const float* img, int pitchf, int rows, int cols,
-                                         int m0, int jp0, int lane) {
-    const int out_cols = p.act == C2D_ACT_GEGLU ? (p.cout >> 1) : p.cout;
+// ROWS x COLS fp32 image -> outputs; picks the 16-B (W = 8) form when the output
+// width, the leading dimensions and the base addresses allow it
+template <int ROWS, int COLS>
+__device__ __forceinline__ void epi_rows(const IgemmParams& p, const float* img, int pitchf, int m0, int jp0,
+                                         int lane) {
+    const bool gg = p.act == C2D_ACT_GEGLU;
+    const int out_cols = gg ? (p.cout >> 1) : p.cout;
     const uintptr_t al = (uintptr_t)p.out | (uintptr_t)p.resid | (uintptr_t)p.temb;
     const bool wide = ((out_cols | p.out_ld | (p.resid ? p.resid_ld : 0) | (p.temb ? p.temb_ld : 0)) & 7) == 0 &&
                       (al & 15) == 0;
-    if (wide) epi_rows_w<8>(p, img, pitchf, rows, cols, m0, jp0, lane);
-    else epi_rows_w<4>(p, img, pitchf, rows, cols, m0, jp0, lane);
+    if constexpr (COLS % 32 == 0) {
+        if (gg) {
+            if (wide) epi_rows_t<8, true, ROWS, COLS>(p, img, pitchf, m0, jp0, lane);
+            else epi_rows_t<4, true, ROWS, COLS>(p, img, pitchf, m0, jp0, lane);
+            return;
+        }
+    }
+    if (wide) epi_rows_t<8, false, ROWS, COLS>(p, img, pitchf, m0, jp0, lane);
+    else epi_rows_t<4, false, ROWS, COLS>(p, img, pitchf, m0, jp0, lane);
 }
 
 }  // namespace c2d

@@ -615,7 +615,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
                         acc[a][b0 + bb];
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
             __builtin_amdgcn_wave_barrier();
-            epi_rows(p, img, PITCHF, RB * 16, TN * 16, mw0 + b0 * 16, nw0, lane);
+            epi_rows<RB * 16, TN * 16>(p, img, PITCHF, mw0 + b0 * 16, nw0, lane);
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
             __builtin_amdgcn_wave_barrier();
         }

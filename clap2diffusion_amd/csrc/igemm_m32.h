@@ -205,8 +205,10 @@ __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x1
                 }
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
             __builtin_amdgcn_wave_barrier();
-            const int nt = (a0 + G <= TN) ? G : TN - a0;
-            epi_rows(p, img, PITCHF, 32, nt * 32, mw0 + b * 32, nw0 + a0 * 32, lane);
+            const int nt = (a0 + G <= TN) ? G : TN - a0;   // folds per unrolled group
+            if (nt == 3) epi_rows<32, 96>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
+            else if (nt == 2) epi_rows<32, 64>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
+            else epi_rows<32, 32>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
             __builtin_amdgcn_wave_barrier();
         }
