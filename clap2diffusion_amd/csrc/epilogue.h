@@ -27,6 +27,8 @@ __device__ __forceinline__ void epi_rows_t(const IgemmParams& p, const float* im
     static_assert(COLS % (GG ? 32 : 8) == 0, "epilogue image width");
     const int hw = p.oh * p.ow;
     const int out_cols = GG ? (p.cout >> 1) : p.cout;
+    // image of all ROWS rows when they cannot straddle one (m0 is a multiple of ROWS)
+    const int n_all = (hw % ROWS) == 0 ? m0 / hw : -1;
 #pragma unroll 2
     for (int c = lane; c < ROWS * CPR; c += 64) {
         const int row = c / CPR, cc = c - row * CPR;
@@ -81,7 +83,7 @@ __device__ __forceinline__ void epi_rows_t(const IgemmParams& p, const float* im
             for (int r = 0; r < W; ++r) v[r] = silu_f(v[r]);
         }
         if (p.temb) {
-            const hv tt = *reinterpret_cast<const hv*>(p.temb + (size_t)(m / hw) * p.temb_ld + j);
+            const hv tt = *reinterpret_cast<const hv*>(p.temb + (size_t)(n_all >= 0 ? n_all : m / hw) * p.temb_ld + j);
 #pragma unroll
             for (int r = 0; r < W; ++r) v[r] += (float)tt[r];
         }

@@ -169,30 +169,53 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict_
 
 // GroupNorm apply (+ SiLU): out[m][c] = act(x[m][c] * scale[n][c] + shift[n][c]),
 // reading a one- or two-source channel concat and writing the concatenation.
-// One 16-B chunk per thread, grid-stride; HBM-bound (2 B read + 2 B written / element).
+// Grid (pixel blocks, image): a thread owns channel chunks lane_c (+ 256 q) of image
+// n, keeps their affine in registers and walks pixels -- no per-chunk index
+// divisions or table reloads.  HBM-bound (2 B read + 2 B written / element).
+template <int CPT>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
-                                                       int c1, int hw, size_t nchunks, const float* __restrict__ scale,
+                                                       int c1, int hw, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int silu, f16* __restrict__ out) {
     const int cin = c0 + c1, nch = cin >> 3;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t pix = i / nch;
-        const int c = (int)(i - pix * nch) * 8;
-        const int n = (int)(pix / hw);
-        const f16* src = (c < c0) ? (s0 + pix * c0 + c) : (s1 + pix * c1 + (c - c0));
-        const f16x8 v = *reinterpret_cast<const f16x8*>(src);
-        const float4* sc = reinterpret_cast<const float4*>(scale + (size_t)n * cin + c);
-        const float4* sh = reinterpret_cast<const float4*>(shift + (size_t)n * cin + c);
-        const float4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
-        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        f16x8 o;
+    const int L = nch < 256 ? nch : 256, R = 256 / L;
+    const int t = threadIdx.x, lane_c = t % L, r0 = t / L;
+    if (r0 >= R) return;
+    const int n = blockIdx.y;
+    const size_t img = (size_t)n * hw;
+    float av[CPT][8], bv[CPT][8];
+    const f16* src[CPT];
+    int ld[CPT], cc[CPT];
+    bool on[CPT];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float y = fmaf((float)v[j], av[j], bv[j]);
-            if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
-            o[j] = (f16)y;
+    for (int q = 0; q < CPT; ++q) {
+        const int ch = lane_c + q * 256;
+        on[q] = ch < nch;
+        cc[q] = (on[q] ? ch : 0) * 8;
+        const int c = cc[q];
+        src[q] = (c < c0) ? (s0 + c) : (s1 + (c - c0));
+        ld[q] = (c < c0) ? c0 : c1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            av[q][i] = scale[(size_t)n * cin + c + i];
+            bv[q][i] = shift[(size_t)n * cin + c + i];
         }
-        *reinterpret_cast<f16x8*>(out + pix * cin + c) = o;
+    }
+#pragma unroll 4
+    for (int pix = blockIdx.x * R + r0; pix < hw; pix += gridDim.x * R) {
+        const size_t gp = img + pix;
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            if (!on[q]) continue;
+            const f16x8 v = *reinterpret_cast<const f16x8*>(src[q] + gp * ld[q]);
+            f16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float y = fmaf((float)v[j], av[q][j], bv[q][j]);
+                if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                o[j] = (f16)y;
+            }
+            *reinterpret_cast<f16x8*>(out + gp * cin + cc[q]) = o;
+        }
     }
 }
 
@@ -434,11 +457,20 @@ extern "C" int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, i
     if ((c0 & 7) || (c1 & 7) || c0 + c1 <= 0 || n <= 0 || hw <= 0) return C2D_E_SHAPE;
     if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out) || !aligned16(scale) || !aligned16(shift))
         return C2D_E_ALIGN;
-    const size_t nchunks = (size_t)n * hw * ((c0 + c1) >> 3);
-    const size_t want = (nchunks + 255) / 256;
-    const unsigned blocks = (unsigned)(want < 8192 ? want : 8192);
-    hipLaunchKernelGGL(gn_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
-                       (const f16*)src1, c0, c1, hw, nchunks, scale, shift, silu, (f16*)out);
+    const int nch = (c0 + c1) >> 3;
+    if (nch > 512) return C2D_E_SHAPE;
+    const int L = nch < 256 ? nch : 256, R = 256 / L;
+    // about 2048 workgroups over the launch, each at least one pass of its rows
+    int bx = (2048 + n - 1) / n;
+    const int maxb = (hw + R - 1) / R;
+    if (bx > maxb) bx = maxb;
+    if (bx < 1) bx = 1;
+    if (nch <= 256)
+        hipLaunchKernelGGL(gn_apply_kernel<1>, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
+                           (const f16*)src1, c0, c1, hw, scale, shift, silu, (f16*)out);
+    else
+        hipLaunchKernelGGL(gn_apply_kernel<2>, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
+                           (const f16*)src1, c0, c1, hw, scale, shift, silu, (f16*)out);
     return check_launch();
 }
 

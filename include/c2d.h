@@ -126,6 +126,7 @@ int c2d_groupnorm_stats(const void* src0, const void* src1, int c0, int c1, int 
  * act = SiLU when silu != 0; the input may be a two-source concat, the output is the
  * concatenation (fp16 [n*hw][c0+c1]).  The UNet materialises each normalised tensor once
  * (HBM-bound) instead of re-normalising it in every 3x3 tap / N-tile of the consuming GEMM.
+ * Limits: c0 + c1 <= 4096.
  */
 int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, int c1, int n, int hw,
                         const float* scale, const float* shift, int silu, void* out, void* stream);
