@@ -360,9 +360,103 @@ __global__ void __launch_bounds__(256) ln_kernel(const f16* __restrict__ x, int 
     }
 }
 
+// LayerNorm + apply with LPR lanes per row and CPL 16-B chunks per lane (the row's
+// C = 8 * LPR * CPL channels in registers): 64 / LPR rows per wave, exact two-pass
+// mean / variance over an LPR-lane xor butterfly, the lane's gamma / beta loaded once
+// and kept across its rows.  The one-wave-per-row kernel left 24 of 64 lanes idle at
+// C = 320 and paid two full-wave reductions per 640-B row.
+template <int LPR, int CPL>
+__global__ void __launch_bounds__(256) ln_rows_kernel(const f16* __restrict__ x, int m, int ld, float eps,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      f16* __restrict__ out, int out_ld) {
+    constexpr int C = 8 * LPR * CPL;
+    constexpr int RPW = 64 / LPR;                    // rows per wave
+    const int lane = threadIdx.x & 63;
+    const int sub = lane % LPR, rw = lane / LPR;
+    const int wave_g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nwaves = gridDim.x * 4;
+    float g[CPL][8], b[CPL][8];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = (sub + k * LPR) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i += 4) {
+            const float4 gg = *reinterpret_cast<const float4*>(gamma + c + i);
+            const float4 bb = *reinterpret_cast<const float4*>(beta + c + i);
+            g[k][i] = gg.x; g[k][i + 1] = gg.y; g[k][i + 2] = gg.z; g[k][i + 3] = gg.w;
+            b[k][i] = bb.x; b[k][i + 1] = bb.y; b[k][i + 2] = bb.z; b[k][i + 3] = bb.w;
+        }
+    }
+    for (int row0 = wave_g * RPW; row0 < m; row0 += nwaves * RPW) {
+        const int row = row0 + rw;
+        const bool ok = row < m;
+        const f16* xr = x + (size_t)(ok ? row : 0) * ld;
+        f16x8 v[CPL];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            v[k] = *reinterpret_cast<const f16x8*>(xr + (sub + k * LPR) * 8);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += (float)v[k][i];
+        }
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) s += __shfl_xor(s, o);
+        const float mean = s * (1.0f / C);
+        float s2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { const float d = (float)v[k][i] - mean; s2 += d * d; }
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) s2 += __shfl_xor(s2, o);
+        const float rstd = rsqrtf(s2 * (1.0f / C) + eps);
+        if (!ok) continue;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            f16x8 o;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] = (f16)(((float)v[k][i] - mean) * rstd * g[k][i] + b[k][i]);
+            *reinterpret_cast<f16x8*>(out + (size_t)row * out_ld + (sub + k * LPR) * 8) = o;
+        }
+    }
+}
+
+// C = 8 * LPR * CPL for LPR in {4, 8, 16, 32}, CPL in {3, 5}: the UNet (320 / 640 / 1280)
+// and HTSAT (96 / 192 / 384 / 768) widths; returns 1 (not launched) when the shape
+// needs the generic kernel, else the launch status
+static int ln_rows_launch(const void* x, int m, int c, int ld, float eps, const float* gamma, const float* beta,
+                          void* out, int out_ld, hipStream_t s) {
+    if ((ld & 7) || (out_ld & 7) || !aligned16(gamma) || !aligned16(beta)) return 1;
+    const int nch = c >> 3;
+    int cpl = 0, lpr = 0;
+    for (int cp : {5, 3}) {
+        if (nch % cp) continue;
+        const int l = nch / cp;
+        if (l == 4 || l == 8 || l == 16 || l == 32) { cpl = cp; lpr = l; break; }
+    }
+    if (!cpl) return 1;
+    const int rows_per_block = 4 * (64 / lpr);
+    long want = ((long)m + rows_per_block - 1) / rows_per_block;
+    const unsigned blocks = (unsigned)(want < 4096 ? want : 4096);
+#define C2D_LNR(L, P)                                                                                            \
+    if (lpr == L && cpl == P) {                                                                                  \
+        hipLaunchKernelGGL((ln_rows_kernel<L, P>), dim3(blocks), dim3(256), 0, s, (const f16*)x, m, ld, eps, gamma, \
+                           beta, (f16*)out, out_ld);                                                             \
+        return check_launch();                                                                                   \
+    }
+    C2D_LNR(4, 3) C2D_LNR(8, 3) C2D_LNR(16, 3) C2D_LNR(32, 3)
+    C2D_LNR(4, 5) C2D_LNR(8, 5) C2D_LNR(16, 5) C2D_LNR(32, 5)
+#undef C2D_LNR
+    return 1;
+}
+
 template <bool APPLY>
 static int ln_dispatch(const void* x, int m, int c, int ld, float eps, float* stats, const float* gamma,
                        const float* beta, void* out, int out_ld, hipStream_t s) {
+    if (APPLY) {
+        const int rc = ln_rows_launch(x, m, c, ld, eps, gamma, beta, out, out_ld, s);
+        if (rc != 1) return rc;
+    }
     const int nch = c >> 3;
     dim3 grid((m + 3) / 4);
     if (nch <= 64)

@@ -451,3 +451,20 @@ def test_m32_vae_width_tiles(dev, n, h, cin, cout):
     wp, kp = ops.pack_conv_weight(w)
     out = ops.conv(nhwc(xh), wp, kp, cout, ksize=3, bias=b.float(), resid=nhwc(rh))
     close(nchw(out), ref)
+
+
+# LayerNorm: the lanes-per-row kernel at the UNet / HTSAT widths (8 * LPR * CPL
+# channels), ragged row counts, a strided input view, and a width that falls back to
+# the one-wave-per-row kernel
+@pytest.mark.parametrize("m,c,ld", [
+    (4099, 320, 320), (1027, 640, 640), (259, 1280, 1280), (333, 96, 96), (97, 768, 768),
+    (130, 320, 960),      # column slice of a wider buffer
+    (77, 136, 136),       # 17 chunks: generic kernel
+])
+def test_layernorm_widths(dev, m, c, ld):
+    base = gen(m, ld, seed=94) * 2 + 0.7
+    gamma, beta = gen(c, seed=95) * 0.1 + 1, gen(c, seed=96) * 0.1
+    xd = base.half().to(dev)[:, :c]
+    ref = F.layer_norm(xd.float().cpu(), (c,), gamma, beta, 1e-5)
+    y = ops.layer_norm(xd, gamma.float().to(dev), beta.float().to(dev), 1e-5)
+    close(y, ref, tol_max=5e-3, tol_l2=1e-3)
