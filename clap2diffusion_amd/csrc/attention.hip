@@ -50,7 +50,12 @@ __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B
     return C::KSW ? row * 128 + ((ch ^ ((row >> 1) & 7)) << 4) : row * C::KS + ch * 16;
 }
 
-template <int D, bool MASK>
+// NEGC: Q is pre-scaled by scale*log2(e) when its fragments load and every S^T tile
+// starts its MFMA chain from C = -m_run (a per-query register block, rewritten only
+// when the running max moves), so the MFMA emits s*scale*log2e - m directly and the
+// softmax is exp2 alone: one v_fma per score less on the VALU issue that bounds the
+// d = 40 kernel.  m_run starts at 0 and the first tile always rebases it to the tile max.
+template <int D, bool MASK, bool NEGC>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
@@ -113,12 +118,25 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
         }
     }
 
+    if (NEGC) {
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) {
+#pragma unroll
+            for (int dc = 0; dc < C::NDC_FULL; ++dc)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) qf[qg][dc][j] = (f16)((float)qf[qg][dc][j] * scale_log2);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) qt[qg][j] = (f16)((float)qt[qg][j] * scale_log2);
+        }
+    }
+
     f32x4 acc[C::NDT][2];
 #pragma unroll
     for (int dt = 0; dt < C::NDT; ++dt)
 #pragma unroll
         for (int qg = 0; qg < 2; ++qg) acc[dt][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+    float m_run[2] = {NEGC ? 0.f : -1e30f, NEGC ? 0.f : -1e30f}, l_run[2] = {0.f, 0.f};
+    f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
     const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
     const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
@@ -171,7 +189,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
                 const f16x8 kf = *reinterpret_cast<const f16x8*>(Ks + k_off<D>(kg * 16 + li, dc * 4 + g));
 #pragma unroll
                 for (int qg = 0; qg < 2; ++qg)
-                    s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], s[qg][kg], 0, 0, 0);
+                    s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc],
+                                                                        (NEGC && dc == 0) ? negm[qg] : s[qg][kg],
+                                                                        0, 0, 0);
             }
 #pragma unroll
             for (int c = 0; c < C::NC16; ++c) {
@@ -216,13 +236,29 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
             mx = fmaxf(mx, __shfl_xor(mx, 32));
             // lazy rescale: the running max only moves (and O, l get rescaled) when
             // some query of the wave gains more than 2^8; otherwise P <= 256 in fp16
-            const float m_cand = fmaxf(m_run[qg], mx * scale_log2);
-            if (__builtin_amdgcn_ballot_w64(m_cand > m_run[qg] + 8.0f)) {
-                const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_cand);
-                m_run[qg] = m_cand;
-                if (!C::SUM_MFMA) l_run[qg] *= alpha;
+            if (NEGC) {
+                // s already holds log2-domain scores minus m_run; the first tile rebases
+                // m_run (0 so far) to the tile max, later ones only move it up
+                if (t == 0 || __builtin_amdgcn_ballot_w64(mx > 8.0f)) {
+                    const float delta = t == 0 ? mx : fmaxf(mx, 0.f);
+                    const float alpha = __builtin_amdgcn_exp2f(-delta);
+                    m_run[qg] += delta;
+                    negm[qg] = (f32x4){-m_run[qg], -m_run[qg], -m_run[qg], -m_run[qg]};
+                    if (!C::SUM_MFMA) l_run[qg] *= alpha;
 #pragma unroll
-                for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
+                    for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
+#pragma unroll
+                    for (int kg = 0; kg < 4; ++kg) s[qg][kg] -= delta;
+                }
+            } else {
+                const float m_cand = fmaxf(m_run[qg], mx * scale_log2);
+                if (__builtin_amdgcn_ballot_w64(m_cand > m_run[qg] + 8.0f)) {
+                    const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_cand);
+                    m_run[qg] = m_cand;
+                    if (!C::SUM_MFMA) l_run[qg] *= alpha;
+#pragma unroll
+                    for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
+                }
             }
             const float m_use = m_run[qg];
             float rs = 0.f;
@@ -230,7 +266,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
             for (int kg = 0; kg < 4; ++kg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], scale_log2, -m_use));
+                    const float pv = NEGC ? __builtin_amdgcn_exp2f(s[qg][kg][r])
+                                          : __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], scale_log2, -m_use));
                     s[qg][kg][r] = pv;
                     if (!C::SUM_MFMA) rs += pv;
                 }
@@ -560,6 +597,12 @@ static int attn_abl() {   // C2D_ATTN_ABL=1: timing ablation of the K/V staging 
     return v;
 }
 
+static bool attn_negc() {   // C2D_ATTN_NEGC=0: the fma-per-score softmax (A/B only)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_ATTN_NEGC"); v = e ? atoi(e) : 1; }
+    return v != 0;
+}
+
 static int attn_pipelined() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
@@ -587,14 +630,18 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
             return check_launch();
         }
     }
-    if (lk % 64 == 0)
-        hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
-                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb,
-                           attn_abl());
-    else
-        hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, ldk,
-                           (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb,
-                           attn_abl());
+#define C2D_ATTN_LAUNCH(MASK, NEGC)                                                                             \
+    hipLaunchKernelGGL((attn_fwd_kernel<D, MASK, NEGC>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, \
+                       ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb, \
+                       attn_abl())
+    // NEGC pays its Q pre-scale and peeled first tile back only over several key tiles
+    // (measured: 4096 keys d = 40 681 -> 646 us, d = 80 75.7 -> 72.6; 77 keys 35.8 -> 38.4)
+    const bool mask = lk % 64 != 0, negc = attn_negc() && lk >= 256;
+    if (!mask && negc) C2D_ATTN_LAUNCH(false, true);
+    else if (!mask) C2D_ATTN_LAUNCH(false, false);
+    else if (negc) C2D_ATTN_LAUNCH(true, true);
+    else C2D_ATTN_LAUNCH(true, false);
+#undef C2D_ATTN_LAUNCH
     return check_launch();
 }
 

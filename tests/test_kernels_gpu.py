@@ -334,6 +334,20 @@ def test_attention_spike(dev):
     close(out, ref)
 
 
+@pytest.mark.parametrize("d", [40, 80, 160])
+def test_attention_wide_scores(dev, d):
+    # scores of std ~12 (log2 units ~17): the first key tile rebases the running max
+    # and later tiles rescale often; ragged lk exercises the masked tail tile
+    b, h, lq, lk = 1, 4, 192, 333
+    q = gen(b * lq, h * d, seed=44) * 12.0
+    k = gen(b * lk, h * d, seed=45)
+    v = gen(b * lk, h * d, seed=46)
+    k[5] -= 3.0  # a strongly negative early key
+    ref = attn_ref(q, k, v, b, h, lq, lk, d)
+    out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d)
+    close(out, ref)
+
+
 def test_groupnorm_large_mean(dev):
     n, c, hw = 2, 640, 1024
     x = gen(n, c, 32, 32, seed=43) + 30.0
