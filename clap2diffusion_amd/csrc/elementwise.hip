@@ -134,6 +134,60 @@ __global__ void l2norm_kernel(float* x, int m, int c) {
     for (int j = threadIdx.x; j < c; j += blockDim.x) x[(size_t)row * c + j] *= inv;
 }
 
+// Row softmax for the materialised single-head attention of the VAE mid block
+// (diffusers Attention with one 512-wide head: softmax(Q K^T / sqrt(d)) over 4096 /
+// 9216 keys; the 1/sqrt(d) is folded into to_q).  One 256-thread workgroup per row,
+// the row held in registers (NCH 16-B chunks per thread): fp32 max, exp2, sum, scale,
+// fp16 out -- one HBM read and one write per score.
+template <int NCH>
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const f16* x, int cols, int ld, f16* out, int ldo) {
+    const size_t row = blockIdx.x;
+    const int tid = threadIdx.x;
+    __shared__ float part[4];
+    f16x8 v[NCH];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int c0 = (i * 256 + tid) * 8;
+        if (c0 < cols) {
+            v[i] = *reinterpret_cast<const f16x8*>(x + row * ld + c0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mx = fmaxf(mx, (float)v[i][j]);
+        }
+    }
+    mx = wave_max(mx);
+    if ((tid & 63) == 0) part[tid >> 6] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(part[0], part[1]), fmaxf(part[2], part[3]));
+    __syncthreads();
+    const float L2E = 1.4426950408889634f, ml = mx * L2E;
+    float e[NCH][8];
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int c0 = (i * 256 + tid) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            e[i][j] = c0 < cols ? __builtin_amdgcn_exp2f(fmaf((float)v[i][j], L2E, -ml)) : 0.f;
+            sum += e[i][j];
+        }
+    }
+    sum = wave_sum(sum);
+    if ((tid & 63) == 0) part[tid >> 6] = sum;
+    __syncthreads();
+    const float inv = 1.0f / (part[0] + part[1] + part[2] + part[3]);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+        const int c0 = (i * 256 + tid) * 8;
+        if (c0 < cols) {
+            f16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = (f16)(e[i][j] * inv);
+            *reinterpret_cast<f16x8*>(out + row * ldo + c0) = o;
+        }
+    }
+}
+
 }  // namespace c2d
 
 using namespace c2d;
@@ -240,5 +294,21 @@ extern "C" int c2d_row_mean(const void* x, int b, int rows, int c, int ld, float
 extern "C" int c2d_l2_normalize(float* x, int m, int c, void* stream) {
     if (!x) return C2D_E_ARG;
     hipLaunchKernelGGL(l2norm_kernel, dim3(m), dim3(256), 0, (hipStream_t)stream, x, m, c);
+    return check_launch();
+}
+
+extern "C" int c2d_softmax_rows(const void* x, int rows, int cols, int ld, void* out, int ldo, void* stream) {
+    if (!x || !out) return C2D_E_ARG;
+    if (rows < 0 || cols <= 0 || cols % 8 || cols > 16384 || ld < cols || ldo < cols) return C2D_E_SHAPE;
+    if (((uintptr_t)x | (uintptr_t)out) & 15 || ld % 8 || ldo % 8) return C2D_E_ALIGN;
+    if (rows == 0) return 0;
+    const int nch = (cols / 8 + 255) / 256;
+    const hipStream_t s = (hipStream_t)stream;
+#define C2D_SM(N) hipLaunchKernelGGL(softmax_rows_kernel<N>, dim3(rows), dim3(256), 0, s, (const f16*)x, cols, ld, (f16*)out, ldo)
+    if (nch <= 1) C2D_SM(1);
+    else if (nch <= 2) C2D_SM(2);
+    else if (nch <= 4) C2D_SM(4);
+    else C2D_SM(8);
+#undef C2D_SM
     return check_launch();
 }

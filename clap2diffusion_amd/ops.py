@@ -238,6 +238,17 @@ def row_mean(x: torch.Tensor, b: int, rows: int) -> torch.Tensor:
     return out
 
 
+def softmax_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Row softmax of a 2-D fp16 matrix (c2d_softmax_rows); out may alias x."""
+    _require(x, "x")
+    assert x.dim() == 2 and x.dtype == F16 and x.stride(1) == 1
+    out = torch.empty_like(x) if out is None else out
+    assert out.shape == x.shape and out.stride(1) == 1
+    check(lib().c2d_softmax_rows(ptr(x), x.shape[0], x.shape[1], x.stride(0), ptr(out), out.stride(0),
+                                 stream_ptr()), "c2d_softmax_rows")
+    return out
+
+
 def l2_normalize_(x: torch.Tensor) -> torch.Tensor:
     m, c = x.shape
     check(lib().c2d_l2_normalize(ptr(x), m, c, stream_ptr()), "c2d_l2_normalize")

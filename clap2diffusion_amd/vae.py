@@ -3,7 +3,8 @@
 SURVEY.md §8(f) "next" #1.  Convolutions, GroupNorm(+SiLU) and the resnet /
 upsample structure reuse the UNet's HIP kernels (NHWC fp16, implicit GEMM with
 fused GN prologue and residual epilogue); the single-head d=512 mid-block
-attention runs through torch SDPA on the HIP-produced Q/K/V for now.
+attention is materialised per image on the same GEMM kernel (S = Q K^T, HIP row
+softmax, O = P V) -- a 512-wide head does not fit the flash kernel's registers.
 diffusers-0.23.1 AutoencoderKL decoder keys (post_quant_conv.*, decoder.*).
 """
 from __future__ import annotations
@@ -21,26 +22,44 @@ SCALING = 0.18215
 
 
 class VAEAttention(nn.Module):
+    """diffusers Attention(c, heads=1, dim_head=c) with its GroupNorm, as in the
+    AutoencoderKL mid block: x + to_out(softmax(q k^T / sqrt(c)) v)."""
+
     def __init__(self, c: int, groups: int = 32):
         super().__init__()
         self.c = c
         self.group_norm = HGroupNorm(groups, c, 1e-6)
         self.to_q, self.to_k, self.to_v = HLinear(c, c), HLinear(c, c), HLinear(c, c)
         self.to_out = nn.ModuleList([HLinear(c, c)])
-        self.register_buffer("w_qkv", torch.zeros(3 * c, ops.kpad_of(c), dtype=torch.float16), persistent=False)
-        self.register_buffer("b_qkv", torch.zeros(3 * c), persistent=False)
+        # to_q with the 1/sqrt(c) score scale folded in (keeps fp16 scores 22x away from overflow)
+        self.register_buffer("w_qs", torch.zeros(c, ops.kpad_of(c), dtype=torch.float16), persistent=False)
+        self.register_buffer("b_qs", torch.zeros(c), persistent=False)
 
     @torch.no_grad()
     def finalize(self):
-        self.w_qkv.copy_(torch.cat([self.to_q.weight, self.to_k.weight, self.to_v.weight]))
-        self.b_qkv.copy_(torch.cat([self.to_q.bias, self.to_k.bias, self.to_v.bias]))
+        sc = self.c ** -0.5
+        self.w_qs.copy_((self.to_q.weight.float() * sc).half())
+        self.b_qs.copy_(self.to_q.bias * sc)
 
     def forward(self, x):
         b, h, w, c = x.shape
-        qkv = ops.conv(self.group_norm.apply(x), self.w_qkv, ops.kpad_of(c), 3 * c, ksize=1, bias=self.b_qkv)
-        qkv = qkv.view(b, 1, h * w, 3 * c)
-        o = F.scaled_dot_product_attention(qkv[..., :c], qkv[..., c:2 * c], qkv[..., 2 * c:])
-        return self.to_out[0](o.reshape(b * h * w, c).contiguous(), resid=x.view(b * h * w, c)).view(b, h, w, c)
+        hw = h * w
+        assert hw % 64 == 0 and c % 64 == 0, "VAE attention needs h*w and c multiples of 64"
+        xn = self.group_norm.apply(x).view(b * hw, c)
+        q = ops.conv(xn, self.w_qs, c, c, ksize=1, bias=self.b_qs)
+        k = ops.conv(xn, self.to_k.weight, c, c, ksize=1, bias=self.to_k.bias)
+        o = torch.empty_like(q)
+        vt = torch.empty(c, hw, device=x.device, dtype=torch.float16)
+        s = torch.empty(hw, hw, device=x.device, dtype=torch.float16)
+        for i in range(b):
+            rows = slice(i * hw, (i + 1) * hw)
+            # V^T = W_v X^T: X is the "weight" operand, so the product lands transposed;
+            # b_v rides the PV epilogue instead (softmax rows sum to 1)
+            ops.conv(self.to_v.weight, xn[rows], c, hw, ksize=1, out=vt)
+            ops.conv(q[rows], k[rows], c, hw, ksize=1, out=s)
+            ops.softmax_rows(s, out=s)
+            ops.conv(s, vt, hw, c, ksize=1, bias=self.to_v.bias, out=o[rows])
+        return self.to_out[0](o, resid=x.view(b * hw, c)).view(b, h, w, c)
 
 
 class VAEDecoder(nn.Module):

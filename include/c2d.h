@@ -208,6 +208,14 @@ int c2d_row_mean(const void* x, int b, int rows, int c, int ld, float* out, void
 /* Row-wise L2 normalise fp32 [m][c] in place (F.normalize, modeling_clap.py:1533). */
 int c2d_l2_normalize(float* x, int m, int c, void* stream);
 
+/* Row softmax fp16 [rows][cols] (leading dims ld / ldo, elements) -> fp16, fp32 math;
+ * cols % 8 == 0, cols <= 16384, 16-B aligned rows.  The score normalisation of the
+ * materialised single-head attention in the VAE decoder's mid block (diffusers
+ * Attention(512, heads=1) inside UNetMidBlock2D of AutoencoderKL; diffusers 0.23.1 is
+ * absent from the reference tree, which loads it through scripts/inference.py:30-33).
+ * May run in place (out == x, ldo == ld). */
+int c2d_softmax_rows(const void* x, int rows, int cols, int ld, void* out, int ldo, void* stream);
+
 /*
  * Sinusoidal timestep embedding of diffusers get_timestep_embedding with
  * flip_sin_to_cos=True, downscale_freq_shift=0: out fp16 [n][dim] = [cos, sin](t*f_i).

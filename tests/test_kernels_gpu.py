@@ -482,3 +482,36 @@ def test_layernorm_widths(dev, m, c, ld):
     ref = F.layer_norm(xd.float().cpu(), (c,), gamma, beta, 1e-5)
     y = ops.layer_norm(xd, gamma.float().to(dev), beta.float().to(dev), 1e-5)
     close(y, ref, tol_max=5e-3, tol_l2=1e-3)
+
+
+@pytest.mark.parametrize("rows,cols,scale", [(64, 4096, 8.0), (33, 9216, 4.0), (5, 264, 1.0), (3, 16384, 2.0)])
+def test_softmax_rows(dev, rows, cols, scale):
+    x = gen(rows, cols, seed=47, scale=scale)
+    ref = torch.softmax(x.half().float(), dim=1)
+    out = ops.softmax_rows(x.half().to(dev))
+    close(out, ref)
+    assert ((out.float().sum(1).cpu() - 1).abs() < 1e-2).all()
+
+
+@pytest.mark.parametrize("b,h,w", [(2, 16, 16), (1, 8, 8)])
+def test_vae_attention(dev, b, h, w):
+    # AutoencoderKL mid-block attention (GN 32 groups eps 1e-6, one 512-wide head) vs fp32 torch
+    from clap2diffusion_amd.vae import VAEAttention
+    c = 512
+    x = gen(b, h, w, c, seed=48)
+    ws = [gen(c, c, seed=50 + i, scale=c ** -0.5) for i in range(4)]
+    bs = [gen(c, seed=60 + i, scale=0.1) for i in range(4)]
+    gam, bet = 1 + gen(c, seed=70, scale=0.1), gen(c, seed=71, scale=0.1)
+    m = VAEAttention(c)
+    m.group_norm.load(gam, bet)
+    for lin, wt, bi in zip([m.to_q, m.to_k, m.to_v, m.to_out[0]], ws, bs):
+        lin.load(wt, bi)
+    m.finalize()
+    m.to(dev)
+    xh = x.half().float()
+    xn = F.group_norm(xh.permute(0, 3, 1, 2), 32, gam, bet, 1e-6).permute(0, 2, 3, 1).reshape(b, h * w, c)
+    q, k, v = (F.linear(xn, wt, bi) for wt, bi in zip(ws[:3], bs[:3]))
+    o = F.scaled_dot_product_attention(q, k, v)
+    ref = (F.linear(o, ws[3], bs[3]).view(b, h, w, c) + xh)
+    out = m(x.half().to(dev))
+    close(out, ref)
