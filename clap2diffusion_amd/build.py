@@ -20,7 +20,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libc2d_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip"]
+SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip", "audio.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I", str(ROOT / "include")]
 # attention rescales its MFMA accumulators with VALU every tile: keep them in

@@ -1,0 +1,105 @@
+"""CLAP log-mel front end on the GPU (c2d_clap_log_mel).
+
+Does the work the reference hands to transformers' ClapProcessor /
+ClapFeatureExtractor (models/audio_encoder.py:163-167, truncation "rand_trunc",
+padding "repeatpad"): waveforms in, [B, 1001, 64] fp32 dB log-mel features out,
+on device, ready for the HTSAT tower.  The host keeps only what is host work in
+the extractor too: the random crop of clips longer than max_length
+(np.random.randint, feature_extraction_clap.py _get_input_mel) and the constant
+tables (periodic Hann window, Slaney mel filter bank of audio_utils.mel_filter_bank)
+built once at construction.  The STFT, power, mel projection and dB run in one
+HIP kernel; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr
+
+
+def _hz_to_mel_slaney(f):
+    f = np.asarray(f, dtype=np.float64)
+    m = 3.0 * f / 200.0
+    log = f >= 1000.0
+    return np.where(log, 15.0 + np.log(np.maximum(f, 1e-30) / 1000.0) * (27.0 / np.log(6.4)), m)
+
+
+def _mel_to_hz_slaney(m):
+    m = np.asarray(m, dtype=np.float64)
+    f = 200.0 * m / 3.0
+    log = m >= 15.0
+    return np.where(log, 1000.0 * np.exp((np.log(6.4) / 27.0) * (m - 15.0)), f)
+
+
+def slaney_mel_filters(n_bins: int, n_mels: int, fmin: float, fmax: float, sr: int) -> np.ndarray:
+    """[n_bins, n_mels] triangular filters, Slaney scale and area norm
+    (transformers audio_utils.mel_filter_bank(norm="slaney", mel_scale="slaney"))."""
+    mel_pts = np.linspace(_hz_to_mel_slaney(fmin), _hz_to_mel_slaney(fmax), n_mels + 2)
+    hz = _mel_to_hz_slaney(mel_pts)
+    fft_freqs = np.linspace(0, sr // 2, n_bins)
+    diff = np.diff(hz)
+    slopes = hz[None, :] - fft_freqs[:, None]
+    down = -slopes[:, :-2] / diff[:-1]
+    up = slopes[:, 2:] / diff[1:]
+    fb = np.maximum(0.0, np.minimum(down, up))
+    return fb * (2.0 / (hz[2:n_mels + 2] - hz[:n_mels]))[None, :]
+
+
+class ClapLogMel:
+    """Device-side ClapFeatureExtractor(truncation="rand_trunc", padding="repeatpad")."""
+
+    def __init__(self, device, feature_size: int = 64, sampling_rate: int = 48_000, hop_length: int = 480,
+                 max_length_s: int = 10, fft_window_size: int = 1024, frequency_min: float = 0.0,
+                 frequency_max: float = 14_000.0):
+        self.device = torch.device(device)
+        self.n_mels, self.sr, self.hop, self.n_fft = feature_size, sampling_rate, hop_length, fft_window_size
+        self.max_len = max_length_s * sampling_rate
+        self.frames = 1 + self.max_len // hop_length
+        n_bins = fft_window_size // 2 + 1
+        fb = slaney_mel_filters(n_bins, feature_size, frequency_min, frequency_max, sampling_rate)  # [bins, mels]
+        nz = fb > 0
+        rng = np.stack([nz.argmax(0), n_bins - nz[::-1].argmax(0)], 1).astype(np.int32)
+        rng[~nz.any(0)] = 0
+        win = np.hanning(fft_window_size + 1)[:-1]                # periodic Hann (audio_utils.window_function)
+        self.window = torch.from_numpy(win.astype(np.float32)).to(self.device)
+        self.filters = torch.from_numpy(np.ascontiguousarray(fb.T).astype(np.float32)).to(self.device)
+        self.filter_range = torch.from_numpy(rng).to(self.device)
+
+    def crop(self, audios: list) -> list:
+        """Host part of _get_input_mel: random crop of clips longer than max_length."""
+        out = []
+        for a in audios:
+            a = np.asarray(a, dtype=np.float32).reshape(-1)
+            if a.size == 0:
+                raise ValueError("empty waveform")
+            if a.size > self.max_len:
+                idx = np.random.randint(0, a.size - self.max_len + 1)
+                a = a[idx: idx + self.max_len]
+            out.append(a)
+        return out
+
+    def __call__(self, audios: list, out: torch.Tensor | None = None) -> torch.Tensor:
+        clips = self.crop(audios)
+        lengths = np.array([c.size for c in clips], dtype=np.int32)
+        offsets = np.concatenate([[0], np.cumsum(lengths[:-1], dtype=np.int64)]).astype(np.int64)
+        wave = torch.from_numpy(np.concatenate(clips)).to(self.device)
+        return self.from_device(wave, torch.from_numpy(offsets).to(self.device),
+                                torch.from_numpy(lengths).to(self.device), out)
+
+    def from_device(self, wave: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
+                    out: torch.Tensor | None = None) -> torch.Tensor:
+        """wave fp32 (clips concatenated, already cropped), offsets int64 [B], lengths int32 [B],
+        all on device -> features fp32 [B, frames, n_mels]."""
+        b = offsets.numel()
+        assert wave.dtype == torch.float32 and offsets.dtype == torch.int64 and lengths.dtype == torch.int32
+        if out is None:
+            out = torch.empty(b, self.frames, self.n_mels, device=self.device, dtype=torch.float32)
+        assert out.shape == (b, self.frames, self.n_mels) and out.is_contiguous()
+        check(lib().c2d_clap_log_mel(ptr(wave), ptr(offsets), ptr(lengths), b, self.max_len, self.n_fft, self.hop,
+                                     ptr(self.window), ptr(self.filters), ptr(self.filter_range), self.n_mels,
+                                     ptr(out), stream_ptr()), "c2d_clap_log_mel")
+        return out
+
+
+__all__ = ["ClapLogMel", "slaney_mel_filters"]

@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from . import weights as W
+from .features import ClapLogMel
 from .htsat import HTSATEncoder
 from .processor import AudioProcessorManager
 from .projectors import AudioAdapter, HierarchicalAudioV4, ImprovedHierarchicalAudioEncoder, normalize_tokens
@@ -111,8 +112,8 @@ class AudioToImageInference:
         self.vae = VAEDecoder().to(dev)
         self.vae.load_diffusers_state_dict(W.synth_vae_decoder(self.seed))
         self.scheduler = DDIMScheduler()
-        from transformers import ClapFeatureExtractor
-        self.feature_extractor = ClapFeatureExtractor(truncation="rand_trunc", padding="repeatpad")
+        # the reference's ClapProcessor feature extraction (models/audio_encoder.py:163-167) on the GPU
+        self.feature_extractor = ClapLogMel(dev)
 
     # ------------------------------------------------------------ reference API
     def load_audio(self, audio_path, duration=10):
@@ -128,8 +129,7 @@ class AudioToImageInference:
         return audio / (np.abs(audio).max() + 1e-8)
 
     def mel_features(self, audios: list) -> torch.Tensor:
-        f = self.feature_extractor(audios, sampling_rate=SR, return_tensors="np")["input_features"]
-        return torch.from_numpy(f[:, 0]).to(self.device)  # [B, 1001, 64]
+        return self.feature_extractor(audios)  # [B, 1001, 64] fp32 on device
 
     def extract_clap_embedding(self, audio) -> torch.Tensor:
         audios = audio if isinstance(audio, list) else [audio]

@@ -208,6 +208,19 @@ int c2d_row_mean(const void* x, int b, int rows, int c, int ld, float* out, void
 /* Row-wise L2 normalise fp32 [m][c] in place (F.normalize, modeling_clap.py:1533). */
 int c2d_l2_normalize(float* x, int m, int c, void* stream);
 
+/* CLAP log-mel front end (transformers ClapFeatureExtractor, truncation "rand_trunc",
+ * padding "repeatpad": feature_extraction_clap.py _get_input_mel + audio_utils.spectrogram
+ * with a periodic Hann window, centre reflect pad, power 2, mel filters, dB; called from
+ * the reference's models/audio_encoder.py:163-167).  wave: fp32 clips concatenated,
+ * clip i at wave + offsets[i] with lengths[i] (1 <= len <= max_len; a longer clip is
+ * cropped by the caller with the extractor's np.random.randint offset).  window fp32
+ * [n_fft]; mel_filters fp32 [n_mels][n_fft/2+1]; filter_range int [n_mels][2] = the
+ * non-zero bin range [lo, hi) of each filter.  out fp32 [b][1 + max_len/hop][n_mels].
+ * n_fft must be 1024. */
+int c2d_clap_log_mel(const float* wave, const long long* offsets, const int* lengths, int b, int max_len,
+                     int n_fft, int hop, const float* window, const float* mel_filters,
+                     const int* filter_range, int n_mels, float* out, void* stream);
+
 /* Row softmax fp16 [rows][cols] (leading dims ld / ldo, elements) -> fp16, fp32 math;
  * cols % 8 == 0, cols <= 16384, 16-B aligned rows.  The score normalisation of the
  * materialised single-head attention in the VAE decoder's mid block (diffusers
