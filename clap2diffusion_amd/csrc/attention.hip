@@ -345,6 +345,53 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q
     }
 }
 
+// Short-sequence attention (L <= 128 keys, d = 64) with an optional causal mask:
+// the CLIP ViT-L/14 text tower (77 tokens, 12 heads; transformers CLIPAttention with
+// its causal mask) that produces SD1.5's encoder_hidden_states once per request.
+// One workgroup per (image, head): K and V of the head staged in LDS (read as
+// broadcasts: every thread walks the same key at the same time), one
+// thread per query with its row in registers and an exact online softmax in fp32.
+// ~0.6 MFLOP per (image, head): latency work, not worth an MFMA tile.
+template <int D>
+__global__ void __launch_bounds__(128) attn_small_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
+                                                         int ldk, const f16* __restrict__ v, int ldv,
+                                                         f16* __restrict__ o, int ldo, int heads, int l, float scale,
+                                                         int causal) {
+    __shared__ f16 ks[128][D], vs[128][D];
+    const int bh = blockIdx.x, b = bh / heads, h = bh - b * heads;
+    const int tid = threadIdx.x;
+    for (int idx = tid; idx < l * D; idx += 128) {
+        const int j = idx / D, c = idx - j * D;
+        ks[j][c] = k[((size_t)b * l + j) * ldk + h * D + c];
+        vs[j][c] = v[((size_t)b * l + j) * ldv + h * D + c];
+    }
+    __syncthreads();
+    if (tid >= l) return;
+    float qr[D], acc[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+        qr[c] = (float)q[((size_t)b * l + tid) * ldq + h * D + c] * scale;
+        acc[c] = 0.f;
+    }
+    float m = -INFINITY, s = 0.f;
+    const int jn = causal ? tid + 1 : l;
+    for (int j = 0; j < jn; ++j) {
+        float d = 0.f;
+#pragma unroll
+        for (int c = 0; c < D; ++c) d = fmaf(qr[c], (float)ks[j][c], d);
+        const float mn = fmaxf(m, d);
+        const float a = __expf(m - mn), p = __expf(d - mn);
+        s = s * a + p;
+#pragma unroll
+        for (int c = 0; c < D; ++c) acc[c] = fmaf(acc[c], a, p * (float)vs[j][c]);
+        m = mn;
+    }
+    const float inv = 1.0f / s;
+    f16* orow = o + ((size_t)b * l + tid) * ldo + h * D;
+#pragma unroll
+    for (int c = 0; c < D; ++c) orow[c] = (f16)(acc[c] * inv);
+}
+
 // ---------------------------------------------------------------------------
 // Software-pipelined variant for d <= 64 (DP = 64: d = 40, 64).  Same fragment
 // layouts as attn_fwd_kernel, but K/V tiles are double-buffered in LDS and each
@@ -720,5 +767,17 @@ extern "C" int c2d_window_attention(const void* qkv, int ld_qkv, const int* row_
     hipLaunchKernelGGL(window_attn_kernel, dim3(n_windows * heads), dim3(64), 0, (hipStream_t)stream,
                        (const f16*)qkv, ld_qkv, row_map, heads, d, bias, mask, n_mask, (f16*)out, ldo,
                        1.0f / sqrtf((float)d));
+    return check_launch();
+}
+
+extern "C" int c2d_attention_small(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                                   int ldo, int batch, int heads, int l, int d, float scale, int causal,
+                                   void* stream) {
+    if (!q || !k || !v || !o) return C2D_E_ARG;
+    if (d != 64 || l <= 0 || l > 128 || batch < 0 || heads <= 0) return C2D_E_SHAPE;
+    if (batch == 0) return 0;
+    hipLaunchKernelGGL(attn_small_kernel<64>, dim3(batch * heads), dim3(128), 0, (hipStream_t)stream,
+                       (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, l, scale,
+                       causal);
     return check_launch();
 }

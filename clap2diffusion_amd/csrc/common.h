@@ -33,6 +33,8 @@ inline int check_launch() {
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(k x): SiLU (k = 1) and quick_gelu (k = 1.702, CLIP text MLP)
+__device__ __forceinline__ float sigmoid_lin(float x, float k) { return x / (1.0f + __expf(-k * x)); }
 // erf-form GELU (torch's default, what diffusers' GEGLU / HTSAT's MLP use) with a
 // branch-free erf: Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 -- far below the
 // fp16 rounding of every output it feeds -- in ~14 VALU ops (one rcp, one exp)

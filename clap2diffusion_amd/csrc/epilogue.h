@@ -81,6 +81,9 @@ __device__ __forceinline__ void epi_rows_t(const IgemmParams& p, const float* im
         } else if (p.act == C2D_ACT_SILU) {
 #pragma unroll
             for (int r = 0; r < W; ++r) v[r] = silu_f(v[r]);
+        } else if (p.act == C2D_ACT_QUICK_GELU) {   // CLIP's quick_gelu x * sigmoid(1.702 x)
+#pragma unroll
+            for (int r = 0; r < W; ++r) v[r] = sigmoid_lin(v[r], 1.702f);
         }
         if (p.temb) {
             const hv tt = *reinterpret_cast<const hv*>(p.temb + (size_t)(n_all >= 0 ? n_all : m / hw) * p.temb_ld + j);

@@ -177,6 +177,7 @@ __device__ __forceinline__ void epilogue_tiles(const IgemmParams& p, f32x4 (&acc
                     if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
                     else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
                     else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
+                    else if (p.act == C2D_ACT_QUICK_GELU) v[r] = sigmoid_lin(v[r], 1.702f);
                     if (p.temb) v[r] += (float)tv[b][a][r];
                     if (p.resid) v[r] += (float)rv[b][a][r];
                 }
@@ -649,6 +650,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
             if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
             else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
             else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
+            else if (p.act == C2D_ACT_QUICK_GELU) v[r] = sigmoid_lin(v[r], 1.702f);
             if (p.temb) v[r] += (float)tv[r];
             if (p.resid) v[r] += (float)rv[r];
             o[r] = (f16)v[r];
@@ -903,7 +905,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     if (d->bias && ((uintptr_t)d->bias & 15)) return C2D_E_ALIGN;
     if (d->pro == C2D_PRO_GN && (!d->pro_a || !d->pro_b || (cin & 3))) return C2D_E_ARG;
     if (d->pro == C2D_PRO_LN && (!d->pro_a || !d->gamma || !d->beta)) return C2D_E_ARG;
-    if (d->pro < 0 || d->pro > 3 || d->act < 0 || d->act > 4) return C2D_E_ARG;
+    if (d->pro < 0 || d->pro > 3 || d->act < 0 || d->act > 5) return C2D_E_ARG;
     if (d->stride != 1 && d->stride != 2) return C2D_E_SHAPE;
     if (d->ksize == 1 && (d->stride != 1 || d->up || d->oh != d->h || d->ow != d->w)) return C2D_E_SHAPE;
     if (d->up && d->stride != 1) return C2D_E_SHAPE;

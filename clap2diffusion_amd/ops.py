@@ -207,6 +207,20 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, hea
     return out
 
 
+def attention_small(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, heads: int, l: int, d: int,
+                    causal: bool, scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Short-sequence (l <= 128, d = 64) attention, optionally causal (c2d_attention_small)."""
+    _require(q, "q")
+    if scale is None:
+        scale = 1.0 / math.sqrt(d)
+    if out is None:
+        out = torch.empty((batch * l, heads * d), device=q.device, dtype=F16)
+    rc = lib().c2d_attention_small(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+                                   out.stride(0), batch, heads, l, d, float(scale), int(causal), stream_ptr())
+    check(rc, "c2d_attention_small")
+    return out
+
+
 def window_attention(qkv: torch.Tensor, row_map: torch.Tensor, n_windows: int, heads: int, d: int,
                      bias: torch.Tensor, mask: torch.Tensor | None, out: torch.Tensor) -> torch.Tensor:
     n_mask = mask.shape[0] if mask is not None else 0

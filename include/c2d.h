@@ -44,6 +44,7 @@ extern "C" {
 #define C2D_ACT_GELU 2       /* exact erf GELU */
 #define C2D_ACT_RELU 3
 #define C2D_ACT_SILU 4
+#define C2D_ACT_QUICK_GELU 5 /* x * sigmoid(1.702 x) (CLIP text MLP, transformers ACT2FN["quick_gelu"]) */
 
 /*
  * Implicit-GEMM convolution / linear layer on MFMA (v_mfma_f32_16x16x32_f16).
@@ -207,6 +208,14 @@ int c2d_row_mean(const void* x, int b, int rows, int c, int ld, float* out, void
 
 /* Row-wise L2 normalise fp32 [m][c] in place (F.normalize, modeling_clap.py:1533). */
 int c2d_l2_normalize(float* x, int m, int c, void* stream);
+
+/* Short-sequence attention, l <= 128 keys = queries, d = 64, optional causal mask
+ * (key j visible to query i iff j <= i): the CLIP ViT-L/14 text tower's self-attention
+ * (transformers CLIPAttention + its causal mask, the encoder_hidden_states producer of
+ * the SD1.5 pipeline the reference drives).  Row layout as
+ * c2d_attention_fwd: head h of token t of image b at [b*l + t][h*d ..]. */
+int c2d_attention_small(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
+                        int ldo, int batch, int heads, int l, int d, float scale, int causal, void* stream);
 
 /* CLAP log-mel front end (transformers ClapFeatureExtractor, truncation "rand_trunc",
  * padding "repeatpad": feature_extraction_clap.py _get_input_mel + audio_utils.spectrogram

@@ -9,7 +9,7 @@ import torch
 
 from clap2diffusion_amd import weights as W
 from clap2diffusion_amd.projectors import ImprovedHierarchicalAudioEncoder
-from clap2diffusion_amd.text_encoder import TextEncoder
+from clap2diffusion_amd.text_encoder import clip_text_model
 from oracle.ddim_ref import sample
 from oracle.htsat_ref import htsat_forward
 from oracle.unet_ref import UNetRef
@@ -24,8 +24,7 @@ def reference_images(mel: torch.Tensor, ids_uncond: torch.Tensor, ids_cond: torc
     enc = W.fill_module(ImprovedHierarchicalAudioEncoder(), "improved.", seed).eval()
     _, info = enc(clap, return_all=True)
     audio = {k: torch.cat([v, v], 0) for k, v in info["routed"].items()}
-    te = TextEncoder("cpu", seed=seed, dtype=torch.float32)
-    ehs = te.model(input_ids=torch.cat([ids_uncond, ids_cond], 0).cpu()).last_hidden_state.float()
+    ehs = clip_text_model(seed)(input_ids=torch.cat([ids_uncond, ids_cond], 0).cpu()).last_hidden_state.float()
     procs = {lv: W.synth_processor_weights(lv, seed) for lv in ("early", "mid", "late")}
     unet = UNetRef(W.synth_unet(seed), processors=procs)
     x = sample(unet, latents.float().cpu(), ehs, audio, steps, guidance)

@@ -515,3 +515,27 @@ def test_vae_attention(dev, b, h, w):
     ref = (F.linear(o, ws[3], bs[3]).view(b, h, w, c) + xh)
     out = m(x.half().to(dev))
     close(out, ref)
+
+
+@pytest.mark.parametrize("b,l,causal", [(2, 77, True), (3, 77, False), (1, 128, True), (2, 5, True)])
+def test_attention_small(dev, b, l, causal):
+    h, d = 12, 64
+    qkv = gen(b * l, 3 * h * d, seed=80)
+    c = h * d
+    qh, kh, vh = (qkv[:, i * c:(i + 1) * c].reshape(b, l, h, d).transpose(1, 2) for i in range(3))
+    ref = F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal).transpose(1, 2).reshape(b * l, c)
+    qd = qkv.half().to(dev)
+    out = ops.attention_small(qd[:, :c], qd[:, c:2 * c], qd[:, 2 * c:], b, h, l, d, causal=causal)
+    close(out, ref)
+
+
+def test_clip_text_tower(dev):
+    # HIP CLIP ViT-L/14 text tower vs the seeded transformers CLIPTextModel in fp32
+    from clap2diffusion_amd.text_encoder import TextEncoder, clip_text_model, tokenize
+    ids = tokenize(["", "a beach", "thunder over a dark city street at night"])
+    model = clip_text_model(0)
+    with torch.no_grad():
+        ref = model(input_ids=ids).last_hidden_state
+    out = TextEncoder(dev, model=model)(ids)
+    assert out.shape == ref.shape and out.dtype == torch.float16
+    close(out, ref, tol_max=3e-2, tol_l2=1e-2)
