@@ -16,6 +16,10 @@
 
 namespace c2d {
 
+#ifndef ATTN_WPE
+#define ATTN_WPE 4
+#endif
+
 template <int D> struct AttnCfg {
     // K dim of QK^T: full 32-deep chunks on 16x16x32 MFMAs plus, when the rest is
     // exactly 16 deep (d = 80), one 16x16x16 MFMA into a separate accumulator
@@ -55,8 +59,12 @@ __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B
 // when the running max moves), so the MFMA emits s*scale*log2e - m directly and the
 // softmax is exp2 alone: one v_fma per score less on the VALU issue that bounds the
 // d = 40 kernel.  m_run starts at 0 and the first tile always rebases it to the tile max.
+// d <= 64: held to 128 VGPRs = 4 waves per SIMD (from 140 = 3); the compiler parks two
+// 8-B values in scratch (one L1-resident reload pair per key tile).  d = 80 / 160 would
+// spill hundreds of bytes at that bound, so they keep the free allocation.
 template <int D, bool MASK, bool NEGC>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? ATTN_WPE : 1)))
+attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
                                                        int kv_div, int nqb, int abl) {

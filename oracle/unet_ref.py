@@ -93,8 +93,11 @@ class UNetRef:
         q = q.view(b, lq, h, d).transpose(1, 2)
         k = k.view(b, lk, h, d).transpose(1, 2)
         v = v.view(b, lk, h, d).transpose(1, 2)
-        s = torch.matmul(q, k.transpose(-1, -2)) * (d ** -0.5)
-        o = torch.matmul(s.softmax(-1), v).transpose(1, 2).reshape(b, lq, c)
+        o = torch.empty_like(q)
+        for i in range(0, lq, 2048):   # query blocks: bounded score memory at 96^2 (c5)
+            s = torch.matmul(q[:, :, i:i + 2048], k.transpose(-1, -2)) * (d ** -0.5)
+            o[:, :, i:i + 2048] = torch.matmul(s.softmax(-1), v)
+        o = o.transpose(1, 2).reshape(b, lq, c)
         return self.lin(pre + ".to_out.0", o)
 
     def audio_context(self, level: str, ehs: torch.Tensor, audio: dict | None) -> torch.Tensor:
