@@ -218,13 +218,17 @@ def main():
             roof["traffic"] = None if tr is None else round(tr)
             roof["traffic_source"] = src
         cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline()
+        # BASELINE.json configs: c3 is the default line; other shapes are labelled, not the metric
+        cfg_name = {(512, 8): "c3", (512, 1): "c2", (768, 4): "c5"}.get((a.res, B), "custom")
+        if world > 1 and (a.res, B) == (512, 8):
+            cfg_name = "c4" if world == 8 else "c3-sharded"
         line = {
             "metric": "512x512 images/sec @ 50 DDIM steps, batch=8, 1/2/4/8 MI355X",
             "value": round(value, 4), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
             "data": "synthetic (seeded thunder-like audio, fixed token ids, random-init SD1.5/CLAP weights)",
-            "config": {"workload": f"c3: batch={B}/GPU, {a.ddim_steps} DDIM steps, {a.res}x{a.res}, CFG 7.5, "
+            "config": {"workload": f"{cfg_name}: batch={B}/GPU, {a.ddim_steps} DDIM steps, {a.res}x{a.res}, CFG 7.5, "
                                    "log-mel+HTSAT+projectors+CLIP+UNet+VAE, all-gather of images",
                        "global_batch": B * world, "ddim_steps": a.ddim_steps, "resolution": a.res,
                        "parallelism": f"dp{world}"},
