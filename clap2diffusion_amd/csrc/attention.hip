@@ -62,38 +62,98 @@ __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B
 // d <= 64: held to 128 VGPRs = 4 waves per SIMD (from 140 = 3); the compiler parks two
 // 8-B values in scratch (one L1-resident reload pair per key tile).  d = 80 / 160 would
 // spill hundreds of bytes at that bound, so they keep the free allocation.
-template <int D, bool MASK, bool NEGC>
+// RES (lk <= 128, the 77-key cross-attention): every key tile stays resident in LDS
+// (one slot per tile, staged once) and the workgroup walks `qpb` consecutive 128-query
+// blocks of its (image, head) over them -- the streaming form re-staged K/V and paid
+// the staging latency once per 128 queries for ~6 MFLOP of work.
+template <int D, bool MASK, bool NEGC, bool RES = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? ATTN_WPE : 1)))
 attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
-                                                       int kv_div, int nqb, int abl) {
+                                                       int kv_div, int nqb, int abl, int qpb = 1) {
     using C = AttnCfg<D>;
+    constexpr int SLOT = C::K_BYTES + C::V_BYTES;
+    constexpr int NSLOT = RES ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* Ks = smem;
     char* Vs = smem + C::K_BYTES;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = tile / nqb, qb = tile - bh * nqb;
+    const int qpb_ = RES ? qpb : 1;   // streaming form: one query block (a single-trip loop below)
+    const int ngrp = (nqb + qpb_ - 1) / qpb_;
+    const int bh = tile / ngrp, qgrp = tile - bh * ngrp;
     const int b = bh / heads, h = bh - b * heads;
     const int bk = b / kv_div;
-    const int q0 = qb * 128 + wave * 32;
     const int g = lane >> 4, li = lane & 15;
 
     // zero the K padding columns once (never rewritten) and the V pad columns
-    for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 256) {
-        int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
-        *reinterpret_cast<f16x8*>(Ks + k_off<D>(row, ch)) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; ++sl) {
+        for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 256) {
+            int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
+            *reinterpret_cast<f16x8*>(Ks + sl * SLOT + k_off<D>(row, ch)) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        // V pad columns: zeros, except column D = 1.0 when there is one, so the PV
+        // product also accumulates the softmax row sum (SUM_MFMA)
+        for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 256) {
+            int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
+            f16x8 z = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+            if (ch == C::DCH) z[0] = (f16)1.0f;
+            *reinterpret_cast<f16x8*>(Vs + sl * SLOT + row * C::VS + ch * 16) = z;
+        }
     }
-    // V pad columns: zeros, except column D = 1.0 when there is one, so the PV
-    // product also accumulates the softmax row sum (SUM_MFMA)
-    for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 256) {
-        int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
-        f16x8 z = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
-        if (ch == C::DCH) z[0] = (f16)1.0f;
-        *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = z;
+
+    const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
+    const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
+    f16x8 rk[C::NLD], rv[C::NLD];
+    auto gload = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            const int idx = tid + 256 * i;
+            const int row = idx / C::DCH, ch = idx - row * C::DCH;
+            // keys past lk re-read the last key: their scores are masked to -inf,
+            // so their V rows meet P = 0
+            const int key = min(t * 64 + row, lk - 1);
+            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
+                rk[i] = *reinterpret_cast<const f16x8*>(kbase + (size_t)key * ldk + ch * 8);
+                rv[i] = *reinterpret_cast<const f16x8*>(vbase + (size_t)key * ldv + ch * 8);
+            }
+        }
+    };
+    auto swrite = [&](int sl) {
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            const int idx = tid + 256 * i;
+            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
+                const int row = idx / C::DCH, ch = idx - row * C::DCH;
+                *reinterpret_cast<f16x8*>(Ks + sl * SLOT + k_off<D>(row, ch)) = rk[i];
+                *reinterpret_cast<f16x8*>(Vs + sl * SLOT + row * C::VS + ch * 16) = rv[i];
+            }
+        }
+    };
+
+    const int ntiles = (lk + 63) / 64;
+    if (RES) {
+        gload(0);
+        __syncthreads();  // pad zeroing done before the tiles land
+        swrite(0);
+        if (ntiles > 1) {
+            gload(1);
+            swrite(1);
+        }
+        __syncthreads();
+    } else {
+        gload(0);
+        __syncthreads();  // pad zeroing done before the first tile lands
+        swrite(0);
+        __syncthreads();
     }
+
+    const int qb_end = RES ? min(nqb, (qgrp + 1) * qpb_) : qgrp + 1;
+    for (int qb = qgrp * qpb_; qb < qb_end; ++qb) {
+    const int q0 = qb * 128 + wave * 32;
 
     // Q fragments (B operand of S^T = K Q^T): query q0 + 16 qg + li, d = 32 dc + 8 g .. +7;
     // tail (16x16x16): d = 32 NDC + 4 g .. +3
@@ -146,43 +206,10 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     float m_run[2] = {NEGC ? 0.f : -1e30f, NEGC ? 0.f : -1e30f}, l_run[2] = {0.f, 0.f};
     f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
-    const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
-    const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
-    f16x8 rk[C::NLD], rv[C::NLD];
-    auto gload = [&](int t) {
-#pragma unroll
-        for (int i = 0; i < C::NLD; ++i) {
-            const int idx = tid + 256 * i;
-            const int row = idx / C::DCH, ch = idx - row * C::DCH;
-            // keys past lk re-read the last key: their scores are masked to -inf,
-            // so their V rows meet P = 0
-            const int key = min(t * 64 + row, lk - 1);
-            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
-                rk[i] = *reinterpret_cast<const f16x8*>(kbase + (size_t)key * ldk + ch * 8);
-                rv[i] = *reinterpret_cast<const f16x8*>(vbase + (size_t)key * ldv + ch * 8);
-            }
-        }
-    };
-    auto swrite = [&]() {
-#pragma unroll
-        for (int i = 0; i < C::NLD; ++i) {
-            const int idx = tid + 256 * i;
-            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
-                const int row = idx / C::DCH, ch = idx - row * C::DCH;
-                *reinterpret_cast<f16x8*>(Ks + k_off<D>(row, ch)) = rk[i];
-                *reinterpret_cast<f16x8*>(Vs + row * C::VS + ch * 16) = rv[i];
-            }
-        }
-    };
-
-    const int ntiles = (lk + 63) / 64;
-    gload(0);
-    __syncthreads();  // pad zeroing done before the first tile lands
-    swrite();
-    __syncthreads();
-
     for (int t = 0; t < ntiles; ++t) {
-        if (t + 1 < ntiles && !abl) gload(t + 1);
+        if (!RES && t + 1 < ntiles && !abl) gload(t + 1);
+        const char* Kt = Ks + (RES ? t * SLOT : 0);
+        const char* Vt = Vs + (RES ? t * SLOT : 0);
 
         // ---- S^T tiles: s[qg][kg] holds keys 16 kg + 4 g + r of query li
         f32x4 s[2][4], st[2][4];
@@ -194,7 +221,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
         for (int kg = 0; kg < 4; ++kg) {
 #pragma unroll
             for (int dc = 0; dc < C::NDC_FULL; ++dc) {
-                const f16x8 kf = *reinterpret_cast<const f16x8*>(Ks + k_off<D>(kg * 16 + li, dc * 4 + g));
+                const f16x8 kf = *reinterpret_cast<const f16x8*>(Kt + k_off<D>(kg * 16 + li, dc * 4 + g));
 #pragma unroll
                 for (int qg = 0; qg < 2; ++qg)
                     s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc],
@@ -203,13 +230,13 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
             }
 #pragma unroll
             for (int c = 0; c < C::NC16; ++c) {
-                const f16x4 kt = *reinterpret_cast<const f16x4*>(Ks + (kg * 16 + li) * C::KS + c * 32 + g * 8);
+                const f16x4 kt = *reinterpret_cast<const f16x4*>(Kt + (kg * 16 + li) * C::KS + c * 32 + g * 8);
 #pragma unroll
                 for (int qg = 0; qg < 2; ++qg)
                     s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x16f16(kt, q16[qg][c], s[qg][kg], 0, 0, 0);
             }
             if (C::TAIL) {
-                const f16x4 kt = *reinterpret_cast<const f16x4*>(Ks + (kg * 16 + li) * C::KS + C::NDC * 64 + g * 8);
+                const f16x4 kt = *reinterpret_cast<const f16x4*>(Kt + (kg * 16 + li) * C::KS + C::NDC * 64 + g * 8);
 #pragma unroll
                 for (int qg = 0; qg < 2; ++qg)
                     st[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x16f16(kt, qt[qg], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -297,7 +324,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
             for (int kb = 0; kb < 2; ++kb) {
                 const int qq = li >> 2, pp = li & 3;
                 const int row1 = kb * 32 + g * 4 + qq;
-                const char* a1 = Vs + row1 * C::VS + (dt * 16 + pp * 4) * 2;
+                const char* a1 = Vt + row1 * C::VS + (dt * 16 + pp * 4) * 2;
                 const char* a2 = a1 + 16 * C::VS;
                 s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a1);
                 s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a2);
@@ -317,9 +344,9 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
         // immediates) measured no faster at d = 40, 3 % faster at d = 80 and 10 %
         // slower on the 77-key cross-attention: the cost is the gload / swrite
         // instructions, not the second barrier.
-        if (t + 1 < ntiles && !abl) {
+        if (!RES && t + 1 < ntiles && !abl) {
             __syncthreads();
-            swrite();
+            swrite(0);
             __syncthreads();
         }
     }
@@ -351,6 +378,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
             }
         }
     }
+    }  // query blocks
 }
 
 // Short-sequence attention (L <= 128 keys, d = 64) with an optional causal mask:
@@ -658,6 +686,12 @@ static bool attn_negc() {   // C2D_ATTN_NEGC=0: the fma-per-score softmax (A/B o
     return v != 0;
 }
 
+static bool attn_res() {   // C2D_ATTN_RES=0: stream K/V tiles for short key sequences too (A/B only)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_ATTN_RES"); v = e ? atoi(e) : 1; }
+    return v != 0;
+}
+
 static int attn_pipelined() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
@@ -684,6 +718,23 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
                                    scale * 1.4426950408889634f, kv_div, nqb);
             return check_launch();
         }
+    }
+    if (lk <= 128 && attn_res()) {
+        // K/V resident, several query blocks per workgroup while >= ~1024 workgroups remain
+        const long bhs = (long)batch * heads;
+        int qpb = (int)((bhs * nqb) / 1024);
+        qpb = qpb < 1 ? 1 : qpb > nqb ? nqb : qpb;
+        const int ngrp = (nqb + qpb - 1) / qpb;
+        dim3 g2((unsigned)(ngrp * bhs));
+        if (lk % 64 == 0)
+            hipLaunchKernelGGL((attn_fwd_kernel<D, false, false, true>), g2, dim3(256), 2 * smem, s, (const f16*)q,
+                               ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk,
+                               scale * 1.4426950408889634f, kv_div, nqb, 0, qpb);
+        else
+            hipLaunchKernelGGL((attn_fwd_kernel<D, true, false, true>), g2, dim3(256), 2 * smem, s, (const f16*)q,
+                               ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk,
+                               scale * 1.4426950408889634f, kv_div, nqb, 0, qpb);
+        return check_launch();
     }
 #define C2D_ATTN_LAUNCH(MASK, NEGC)                                                                             \
     hipLaunchKernelGGL((attn_fwd_kernel<D, MASK, NEGC>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, \

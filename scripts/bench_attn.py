@@ -14,6 +14,8 @@ SHAPES = [  # name, batch, heads, lq, lk, d
     ("L0 cross 4096x77 d40", 16, 8, 4096, 77, 40),
     ("L1 self 1024x1024 d80", 16, 8, 1024, 1024, 80),
     ("L2 self 256x256 d160", 16, 8, 256, 256, 160),
+    ("L1 cross 1024x77 d80", 16, 8, 1024, 77, 80),
+    ("L2 cross 256x77 d160", 16, 8, 256, 77, 160),
 ]
 
 

@@ -310,6 +310,8 @@ def attn_ref(q, k, v, b, h, lq, lk, d):
     (2, 8, 256, 256, 40), (2, 8, 200, 77, 40), (2, 8, 1024, 1024, 80), (2, 8, 64, 64, 160),
     (1, 8, 256, 77, 160), (2, 4, 300, 300, 64), (2, 8, 4096, 4096, 40),
     (1, 8, 9216, 9216, 40), (1, 8, 2304, 2304, 80),   # c5: 768^2 images (96^2 latent) levels 0 / 1
+    # resident-K/V path (lk <= 128): several query blocks per workgroup, ragged last block
+    (16, 8, 4000, 77, 40), (16, 8, 1024, 77, 80), (16, 8, 256, 77, 160), (4, 8, 700, 128, 40), (3, 8, 300, 64, 80),
 ])
 def test_attention(dev, b, h, lq, lk, d):
     c = h * d
