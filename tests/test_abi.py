@@ -49,3 +49,28 @@ def test_error_codes_without_gpu():
     ws = L.c2d_groupnorm_workspace_size(2, 320, 4096)   # n * nblk * c * (sum, sumsq) fp32
     assert ws > 0 and ws % (2 * 320 * 2 * 4) == 0 and ws // (2 * 320 * 2 * 4) <= 4096
     assert L.c2d_version().startswith(b"c2d_hip gfx950")
+
+
+def test_new_entry_points_validate_before_launch():
+    """log-mel / short attention / row softmax: documented C2D_E_* codes, nothing launched."""
+    import torch  # noqa: F401
+    from clap2diffusion_amd import _lib
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(64)            # host memory: never dereferenced on these paths
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    # c2d_clap_log_mel: null -> ARG; n_fft != 1024 or max_len <= n_fft/2 -> SHAPE; b == 0 -> OK
+    assert L.c2d_clap_log_mel(None, p, p, 1, 480000, 1024, 480, p, p, p, 64, p, None) == -1
+    assert L.c2d_clap_log_mel(p, p, p, 1, 480000, 2048, 480, p, p, p, 64, p, None) == -2
+    assert L.c2d_clap_log_mel(p, p, p, 1, 400, 1024, 480, p, p, p, 64, p, None) == -2
+    assert L.c2d_clap_log_mel(p, p, p, 0, 480000, 1024, 480, p, p, p, 64, p, None) == 0
+    # c2d_attention_small: d != 64 or l > 128 -> SHAPE; batch 0 -> OK
+    assert L.c2d_attention_small(p, 192, p, 192, p, 192, p, 64, 1, 1, 77, 40, 0.125, 1, None) == -2
+    assert L.c2d_attention_small(p, 192, p, 192, p, 192, p, 64, 1, 1, 129, 64, 0.125, 1, None) == -2
+    assert L.c2d_attention_small(None, 192, p, 192, p, 192, p, 64, 1, 1, 77, 64, 0.125, 1, None) == -1
+    assert L.c2d_attention_small(p, 192, p, 192, p, 192, p, 64, 0, 1, 77, 64, 0.125, 1, None) == 0
+    # c2d_softmax_rows: cols % 8, cols > 16384 -> SHAPE; misaligned ld -> ALIGN; rows 0 -> OK
+    aligned = ctypes.c_void_p((ctypes.addressof(buf) + 15) & ~15)
+    assert L.c2d_softmax_rows(aligned, 4, 12, 16, aligned, 16, None) == -2
+    assert L.c2d_softmax_rows(aligned, 4, 16392, 16392, aligned, 16392, None) == -2
+    assert L.c2d_softmax_rows(aligned, 4, 16, 20, aligned, 16, None) == -3
+    assert L.c2d_softmax_rows(aligned, 0, 16, 16, aligned, 16, None) == 0
