@@ -49,23 +49,42 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
                 shift[q][i] = gn_read(s0, s1, c0, c1, img, (c / cpg) * cpg);
             }
         }
-#pragma unroll 4
-        for (int pix = p_begin + r0; pix < p_end; pix += R) {   // 4 loads in flight per thread
+        auto ld8 = [&](int pix, int q) {
             const size_t gp = img + pix;
+            const int c = (ch_base + q * 256) * 8;
+            const f16* ptr = (c < c0) ? (s0 + gp * c0 + c) : (s1 + gp * c1 + (c - c0));
+            return *reinterpret_cast<const f16x8*>(ptr);
+        };
+        auto acc8 = [&](const f16x8& v, int q) {
 #pragma unroll
-            for (int q = 0; q < CPT; ++q) {
-                const int ch = ch_base + q * 256;
-                if (ch >= nch) continue;
-                const int c = ch * 8;
-                const f16* ptr = (c < c0) ? (s0 + gp * c0 + c) : (s1 + gp * c1 + (c - c0));
-                f16x8 v = *reinterpret_cast<const f16x8*>(ptr);
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    float d = (float)v[i] - shift[q][i];
-                    sum[q][i] += d;
-                    sq[q][i] += d * d;
-                }
+            for (int i = 0; i < 8; ++i) {
+                float d = (float)v[i] - shift[q][i];
+                sum[q][i] += d;
+                sq[q][i] += d * d;
             }
+        };
+        // four pixels per trip, all loads issued before the sums (same per-thread pixel
+        // order as one at a time, so the statistics are bit-identical); chunk 0 always
+        // exists for an active thread, so CPT = 1 has no per-load branch
+        int pix = p_begin + r0;
+        for (; pix + 3 * R < p_end; pix += 4 * R) {
+            f16x8 v[4][CPT];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int q = 0; q < CPT; ++q)
+                    if (q == 0 || ch_base + q * 256 < nch) v[u][q] = ld8(pix + u * R, q);
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int q = 0; q < CPT; ++q)
+                    if (q == 0 || ch_base + q * 256 < nch) acc8(v[u][q], q);
+        }
+        for (; pix < p_end; pix += R) {
+#pragma unroll
+            for (int q = 0; q < CPT; ++q)
+                if (q == 0 || ch_base + q * 256 < nch) acc8(ld8(pix, q), q);
         }
     }
     // block reduction over the R row-threads sharing a channel chunk
