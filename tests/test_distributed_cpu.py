@@ -1,7 +1,9 @@
-"""world_size-2 gloo run of the data-parallel plumbing: sample sharding, per-sample
-seeded latents identical to a single-process run, image all-gather."""
+"""world_size-2 and -4 gloo runs of the data-parallel plumbing: sample sharding, per-sample
+seeded latents identical to a single-process run, image all-gather (bit-identical images
+for any rank count: the 1/2/4/8-GPU scaling runs generate the same samples)."""
 import os
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -27,8 +29,8 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_shard_and_gather():
-    world, port = 2, 29513
+@pytest.mark.parametrize("world,port", [(2, 29513), (4, 29517)])
+def test_rank_shard_and_gather(world, port):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -38,6 +40,6 @@ def test_two_rank_shard_and_gather():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    ref = _latents(range(8))
+    ref = _latents(range(4 * world))
     ref_img = (ref[:, :3].permute(0, 2, 3, 1).abs() * 50).clamp(0, 255).to(torch.uint8).numpy()
     assert (got == ref_img).all()
