@@ -188,6 +188,23 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const f16* x, int col
     }
 }
 
+// Weight prepack: fp32 [cout][cin][k][k] (PyTorch
+// conv / linear layout, k = 1 for a linear) -> fp16 [cout][kpad], K ordered
+// (ky, kx, channel) over cin_pad channels (channels >= cin and K >= k*k*cin_pad are 0).
+__global__ void pack_weights_kernel(const float* __restrict__ w, int cout, int cin, int ksz, int cin_pad, int kpad,
+                                    f16* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)cout * kpad) return;
+    const int o = (int)(i / kpad), kk = (int)(i - (size_t)o * kpad);
+    float v = 0.f;
+    if (kk < ksz * ksz * cin_pad) {
+        const int tap = kk / cin_pad, c = kk - tap * cin_pad;
+        const int ky = tap / ksz, kx = tap - ky * ksz;
+        if (c < cin) v = w[(((size_t)o * cin + c) * ksz + ky) * ksz + kx];
+    }
+    out[i] = (f16)v;
+}
+
 }  // namespace c2d
 
 using namespace c2d;
@@ -310,5 +327,17 @@ extern "C" int c2d_softmax_rows(const void* x, int rows, int cols, int ld, void*
     else if (nch <= 4) C2D_SM(4);
     else C2D_SM(8);
 #undef C2D_SM
+    return check_launch();
+}
+
+extern "C" int c2d_pack_weights(const float* w, int cout, int cin, int ksize, int cin_pad, int kpad, void* out,
+                                void* stream) {
+    if (!w || !out) return C2D_E_ARG;
+    if (cout <= 0 || cin <= 0 || (ksize != 1 && ksize != 3) || cin_pad < cin || kpad % 64 ||
+        kpad < ksize * ksize * cin_pad)
+        return C2D_E_SHAPE;
+    const size_t n = (size_t)cout * kpad;
+    hipLaunchKernelGGL(pack_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w,
+                       cout, cin, ksize, cin_pad, kpad, (f16*)out);
     return check_launch();
 }

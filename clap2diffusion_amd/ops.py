@@ -40,6 +40,20 @@ def pack_conv_weight(w: torch.Tensor, cin_pad: int | None = None) -> tuple[torch
     return wp.to(F16).contiguous(), kp
 
 
+def pack_weights_device(w: torch.Tensor, cin_pad: int | None = None) -> tuple[torch.Tensor, int]:
+    """c2d_pack_weights: the on-device form of pack_conv_weight / pack_linear_weight
+    (fp32 weight already on the GPU -> fp16 [cout][kpad])."""
+    _require(w, "w")
+    w = w.float().contiguous()
+    cout, cin = w.shape[:2]
+    ks = w.shape[2] if w.dim() == 4 else 1
+    cp = max(cin_pad or cin, cin)
+    kp = kpad_of(ks * ks * cp)
+    out = torch.empty(cout, kp, device=w.device, dtype=F16)
+    check(lib().c2d_pack_weights(ptr(w), cout, cin, ks, cp, kp, ptr(out), stream_ptr()), "c2d_pack_weights")
+    return out, kp
+
+
 def pack_linear_weight(w: torch.Tensor) -> tuple[torch.Tensor, int]:
     """[out, in] -> fp16 [out][kpad]."""
     out_f, in_f = w.shape

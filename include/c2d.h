@@ -230,6 +230,14 @@ int c2d_clap_log_mel(const float* wave, const long long* offsets, const int* len
                      int n_fft, int hop, const float* window, const float* mel_filters,
                      const int* filter_range, int n_mels, float* out, void* stream);
 
+/* Weight prepack for c2d_conv2d_igemm: fp32 [cout][cin][ksize][ksize] (PyTorch layout;
+ * ksize 1 for a Linear [cout][cin]) -> fp16 [cout][kpad] with K ordered (ky, kx, channel)
+ * over cin_pad >= cin channels, zero-filled past cin and past ksize^2 * cin_pad;
+ * kpad % 64 == 0.  Replaces the layout work diffusers / transformers never do (their
+ * convs run NCHW through cuDNN / MIOpen); one-time, at checkpoint load. */
+int c2d_pack_weights(const float* w, int cout, int cin, int ksize, int cin_pad, int kpad, void* out,
+                     void* stream);
+
 /* Row softmax fp16 [rows][cols] (leading dims ld / ldo, elements) -> fp16, fp32 math;
  * cols % 8 == 0, cols <= 16384, 16-B aligned rows.  The score normalisation of the
  * materialised single-head attention in the VAE decoder's mid block (diffusers

@@ -542,3 +542,13 @@ def test_clip_text_tower(dev):
     out = TextEncoder(dev, model=model)(ids)
     assert out.shape == ref.shape and out.dtype == torch.float16
     close(out, ref, tol_max=3e-2, tol_l2=1e-2)
+
+
+@pytest.mark.parametrize("cout,cin,k,cin_pad", [(320, 4, 3, 8), (640, 320, 3, None), (1280, 768, 1, None),
+                                                 (77, 100, 1, None), (128, 512, 3, None)])
+def test_pack_weights_matches_host_packer(dev, cout, cin, k, cin_pad):
+    # c2d_pack_weights is bit-identical to the host packer the layers use
+    w = gen(cout, cin, k, k, seed=90) if k == 3 else gen(cout, cin, seed=90)
+    ref, kp_ref = (ops.pack_conv_weight(w, cin_pad=cin_pad) if k == 3 else ops.pack_linear_weight(w))
+    out, kp = ops.pack_weights_device(w.to(dev), cin_pad=cin_pad)
+    assert kp == kp_ref and torch.equal(out.cpu(), ref)
