@@ -28,7 +28,6 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 PEAK_F16_TFLOPS = 2500.0  # MI355X dense fp16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
@@ -111,27 +110,77 @@ def pmc_traffic(timeout_s: int = 120):
                     f"{vals['WRITE_SIZE']:.0f} KiB per launch"
 
 
-def cpu_baseline(calls: int = 2):
-    """The fp32 CPU oracle (oracle/unet_ref.py, a port of the diffusers path the
-    reference glues together) timed on host cores: `calls` CFG-pair UNet calls at
-    512x512 (64x64 latent, N = 2), extrapolated to images/sec at 50 DDIM steps."""
-    from clap2diffusion_amd.weights import synth_unet
-    from oracle.unet_ref import UNetRef
-    cores = min(16, os.cpu_count() or 1)
+def cpu_baseline(cores: int | None = None):
+    """Config c1 of BASELINE.json / BASELINE.md §2 on the host cores: the full fp32 CPU
+    pipeline (oracle/pipeline_ref.py, the port of the diffusers + transformers path the
+    reference glues together): preprocess + log-mel -> HTSAT -> projectors -> CLIP ->
+    10 CFG+DDIM UNet calls at 512^2 (64^2 latent, N = 2) -> VAE decode, B = 1,
+    synthetic "Thunder" clip + "a beach".  One timed run after a one-UNet-call warm-up
+    (a median of 3 would take ~4 minutes); weights are built before the clock starts.
+    The 50-step figure is extrapolated from the measured stage times."""
+    from clap2diffusion_amd.distributed import sample_seed
+    from clap2diffusion_amd.pipeline import initial_latents, synthetic_thunder
+    from clap2diffusion_amd.text_encoder import tokenize
+    from oracle.pipeline_ref import ReferencePipeline
+    cores = cores or min(16, os.cpu_count() or 1)
     torch.set_num_threads(cores)
-    ref = UNetRef(synth_unet(0))
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(2, 4, 64, 64, generator=g)
-    ehs = torch.randn(2, 77, 768, generator=g)
-    with torch.no_grad():
-        ref(x, 981, ehs)  # warm-up
-        t0 = time.time()
-        for i in range(calls):
-            ref(x, 981 - 20 * i, ehs)
-        dt = (time.time() - t0) / calls
-    return {"value": round(1.0 / (dt * 50), 6), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": f"{calls} UNet calls (CFG pair, fp32, 64x64 latent) on {cores} threads = {dt:.2f} s/call, "
-                      f"x50 DDIM steps per image; HTSAT/CLIP/VAE excluded (they add ~3% of the FLOPs)"}
+    ref = ReferencePipeline(0)
+    lat = initial_latents([sample_seed(0, 0)], 64, 64)
+    ids_u, ids_c = tokenize([""]), tokenize(["a beach"])
+    with torch.no_grad():   # warm-up: one CFG-pair UNet call (oneDNN primitive creation)
+        ref.unet(torch.cat([lat, lat]), 981, torch.zeros(2, 77, 768), None)
+    tm = {}
+    ref.run([synthetic_thunder(0)], ids_u, ids_c, lat, 10, 7.5, timings=tm)
+    unet_call = float(np.median(tm["unet"]))
+    fixed = tm["mel"] + tm["condition"] + tm["vae"]
+    s50 = fixed + 50 * unet_call
+    return {"value": round(1.0 / tm["total"], 6), "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": f"config c1: 1 x 512^2, 10 DDIM steps, fp32 CPU pipeline (log-mel, HTSAT, projectors, CLIP, "
+                      f"10 CFG-pair UNet calls, VAE) on {cores} threads, 1 run after warm-up",
+            "c1_seconds_per_image": round(tm["total"], 2),
+            "stage_seconds": {"mel": round(tm["mel"], 3), "condition": round(tm["condition"], 3),
+                              "unet_call_median": round(unet_call, 3), "unet_total": round(sum(tm["unet"]), 2),
+                              "vae": round(tm["vae"], 2)},
+            "images_per_s_50_steps_extrapolated": round(1.0 / s50, 6)}
+
+
+def gpu_config_runs(pipe, dev, log):
+    """The other single-GPU configs of BASELINE.json, measured in the same process after the
+    headline run: c2 (B = 1, 50 steps, 512^2: latency, median of 5 after a warm-up), c1's
+    workload on the GPU (B = 1, 10 steps), c5 (768^2, B = 4, 50 steps: images/s)."""
+    from clap2diffusion_amd.distributed import rank_inputs
+
+    def gen(b, res, steps, reps, warm):
+        inp = rank_inputs(list(range(b)), (res // 8, res // 8), dev)
+        clips = pipe.feature_extractor.crop(inp.audios)
+        wave = torch.from_numpy(np.concatenate(clips)).to(dev)
+        lens = torch.tensor([c.size for c in clips], dtype=torch.int32, device=dev)
+        offs = torch.tensor(np.cumsum([0] + [c.size for c in clips[:-1]]), dtype=torch.int64, device=dev)
+
+        def one():
+            mel = pipe.feature_extractor.from_device(wave, offs, lens)
+            return pipe.generate_batch(mel, None, steps, 7.5, ids=(inp.ids_uncond, inp.ids_cond), latents=inp.latents)
+        for _ in range(warm):
+            one()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            one()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return ts
+
+    out = {}
+    ts = gen(1, 512, 50, 5, 2)
+    out["c2_latency_s"] = round(float(np.median(ts)), 4)
+    log(f"[bench] c2 latency {out['c2_latency_s']} s")
+    ts = gen(1, 512, 10, 5, 2)
+    out["c1_gpu_latency_s"] = round(float(np.median(ts)), 4)
+    ts = gen(4, 768, 50, 2, 1)
+    out["c5_images_per_s"] = round(4 / float(np.mean(ts)), 4)
+    log(f"[bench] c5 {out['c5_images_per_s']} img/s")
+    return out
 
 
 def main():
@@ -144,99 +193,73 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-configs", action="store_true", help="skip the c1/c2/c5 side measurements")
     a = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    from clap2diffusion_amd import distributed as D
+    from clap2diffusion_amd.pipeline import AudioToImageInference
 
-    from clap2diffusion_amd.pipeline import AudioToImageInference, synthetic_thunder
-    from clap2diffusion_amd.text_encoder import tokenize
-
+    ctx = D.init("cuda")
+    dev = ctx.device
     t_setup = time.time()
     pipe = AudioToImageInference(device=dev, height=a.res, width=a.res, verbose=False)
     B = a.batch
-    gidx = [rank * B + i for i in range(B)]  # global sample indices of this rank
-    audios = [synthetic_thunder(i) for i in gidx]
+    inp = D.rank_inputs(ctx.shard(B), (a.res // 8, a.res // 8), dev)
     # waveforms resident in HBM; the log-mel front end (c2d_clap_log_mel) runs inside the step
-    clips = pipe.feature_extractor.crop(audios)
+    clips = pipe.feature_extractor.crop(inp.audios)
     wave = torch.from_numpy(np.concatenate(clips)).to(dev)
     lens = torch.tensor([c.size for c in clips], dtype=torch.int32, device=dev)
     offs = torch.tensor(np.cumsum([0] + [c.size for c in clips[:-1]]), dtype=torch.int64, device=dev)
-    prompts = ["a beach" if i % 2 == 0 else "a city street at night" for i in gidx]
-    ids = (tokenize([""] * B, dev), tokenize(prompts, dev))
-    latents = pipe.initial_latents([i for i in gidx])
-    gathered = [torch.empty(B, a.res, a.res, 3, dtype=torch.uint8, device=dev) for _ in range(world)]
-    if rank == 0:
-        log(f"[bench] setup {time.time() - t_setup:.1f}s, world={world}, batch/gpu={B}")
+    gathered = [torch.empty(B, a.res, a.res, 3, dtype=torch.uint8, device=dev) for _ in range(ctx.world)]
+    if ctx.rank == 0:
+        log(f"[bench] setup {time.time() - t_setup:.1f}s, world={ctx.world}, batch/gpu={B}")
 
     def one_batch():
         mel = pipe.feature_extractor.from_device(wave, offs, lens)
-        img = pipe.generate_batch(mel, None, a.ddim_steps, 7.5, ids=ids, latents=latents)
-        if world > 1:
-            dist.all_gather(gathered, img)
-        else:
-            gathered[0] = img
+        img = pipe.generate_batch(mel, None, a.ddim_steps, 7.5, ids=(inp.ids_uncond, inp.ids_cond),
+                                  latents=inp.latents)
+        ctx.all_gather(img, gathered)
         return img
 
-    for i in range(a.warmup):
-        one_batch()
-        torch.cuda.synchronize()
-        if rank == 0:
-            log(f"[bench] warmup {i} done")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        img = one_batch()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
-    finite = bool(torch.isfinite(pipe._denoisers[(B, a.ddim_steps, 7.5)].x).all().item())
+    dt, _ = D.timed_run(ctx, one_batch, a.steps, a.warmup, torch.cuda.synchronize,
+                        log=lambda m: log("[bench] " + m))
+    finite = bool(torch.isfinite(pipe.last_denoiser.x).all().item())
     ms_per_step = dt / a.steps * 1e3
-    total_images = world * B * a.steps
+    total_images = ctx.world * B * a.steps
     value = total_images / dt
 
-    if rank == 0:
+    if ctx.rank == 0:
         roof = measure_dominant_kernel(dev)
-        unet_tf = UNET_GFLOP_PER_SAMPLE * (a.res / 512) ** 2 * 2 * a.ddim_steps * world * B * a.steps / dt / 1e3
+        unet_tf = UNET_GFLOP_PER_SAMPLE * (a.res / 512) ** 2 * 2 * a.ddim_steps * total_images / dt / 1e3
         roof["pipeline_unet_tflops"] = round(unet_tf, 2)
         n_, h_, c_ = 16, 64, 320
         roof["algorithmic_bytes"] = 2 * (3 * n_ * h_ * h_ * c_ + c_ * 9 * c_)  # x + resid + out + weights
-        if not a.no_pmc and world == 1:
+        if not a.no_pmc and ctx.world == 1:
             tr, src = pmc_traffic()
             roof["traffic"] = None if tr is None else round(tr)
             roof["traffic_source"] = src
-        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline()
+        extra = {}
+        if not a.no_configs and ctx.world == 1 and (a.res, B) == (512, 8):
+            extra = gpu_config_runs(pipe, dev, log)
+        cpu = None if (a.no_cpu_baseline or ctx.world > 1) else cpu_baseline()
         # BASELINE.json configs: c3 is the default line; other shapes are labelled, not the metric
         cfg_name = {(512, 8): "c3", (512, 1): "c2", (768, 4): "c5"}.get((a.res, B), "custom")
-        if world > 1 and (a.res, B) == (512, 8):
-            cfg_name = "c4" if world == 8 else "c3-sharded"
+        if ctx.world > 1 and (a.res, B) == (512, 8):
+            cfg_name = "c4" if ctx.world == 8 else "c3-sharded"
         line = {
             "metric": "512x512 images/sec @ 50 DDIM steps, batch=8, 1/2/4/8 MI355X",
-            "value": round(value, 4), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+            "value": round(value, 4), "unit": "images/sec", "n_gpus": ctx.world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
             "data": "synthetic (seeded thunder-like audio, fixed token ids, random-init SD1.5/CLAP weights)",
             "config": {"workload": f"{cfg_name}: batch={B}/GPU, {a.ddim_steps} DDIM steps, {a.res}x{a.res}, CFG 7.5, "
                                    "log-mel+HTSAT+projectors+CLIP+UNet+VAE, all-gather of images",
-                       "global_batch": B * world, "ddim_steps": a.ddim_steps, "resolution": a.res,
-                       "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "latents_finite": finite,
+                       "global_batch": B * ctx.world, "ddim_steps": a.ddim_steps, "resolution": a.res,
+                       "parallelism": f"dp{ctx.world}"},
+            "roofline": roof, "cpu_baseline": cpu, "latents_finite": finite, **extra,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == "__main__":

@@ -28,9 +28,9 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-at
 EXTRA = {"attention.hip": ["-Xarch_device", "-mllvm=-amdgpu-mfma-vgpr-form=true"]}
 
 
-def _digest() -> str:
+def _digest(defines=()) -> str:
     h = hashlib.sha256()
-    h.update(repr((FLAGS, EXTRA)).encode())
+    h.update(repr((FLAGS, EXTRA, tuple(defines))).encode())
     for f in sorted(CSRC.iterdir()):
         if f.suffix in (".hip", ".h", ".cpp"):
             h.update(f.name.encode())
@@ -40,27 +40,32 @@ def _digest() -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src: str, build_dir: Path) -> Path:
+def _compile(src: str, build_dir: Path, defines=()) -> Path:
     obj = build_dir / (Path(src).stem + ".o")
-    cmd = [HIPCC, *FLAGS, *EXTRA.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], *EXTRA.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
-    stamp = PKG / ".libc2d_hip.stamp"
-    dig = _digest()
-    if LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig and not force:
+def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bool = False) -> Path:
+    """ablation=True builds libc2d_hip_abl.so with -DC2D_ENABLE_ABLATION (timing-ablation
+    switches live; wrong results by design) for scripts/gpu_gemm_abl.sh via C2D_LIB; the
+    production libc2d_hip.so never contains them."""
+    defines = ("C2D_ENABLE_ABLATION",) if ablation else ()
+    lib_path = PKG / ("libc2d_hip_abl.so" if ablation else "libc2d_hip.so")
+    stamp = PKG / (".libc2d_hip_abl.stamp" if ablation else ".libc2d_hip.stamp")
+    dig = _digest(defines)
+    if lib_path.exists() and stamp.exists() and stamp.read_text().strip() == dig and not force:
         if verbose:
-            print(f"[c2d] {LIB.name} up to date ({dig})")
-        return LIB
-    build_dir = ROOT / "build" / "c2d"
+            print(f"[c2d] {lib_path.name} up to date ({dig})")
+        return lib_path
+    build_dir = ROOT / "build" / ("c2d_abl" if ablation else "c2d")
     build_dir.mkdir(parents=True, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, build_dir), SOURCES))
-    tmp = LIB.with_suffix(".so.tmp")
+        objs = list(ex.map(lambda s: _compile(s, build_dir, defines), SOURCES))
+    tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -72,17 +77,18 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
     if bad:
         tmp.unlink()
         raise RuntimeError("undefined device-kernel stubs in libc2d_hip.so:\n  " + "\n  ".join(bad))
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib_path)
     stamp.write_text(dig)
     if verbose:
-        print(f"[c2d] built {LIB} ({dig})")
-    return LIB
+        print(f"[c2d] built {lib_path} ({dig})")
+    return lib_path
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=4)
+    ap.add_argument("--ablation", action="store_true", help="build libc2d_hip_abl.so (timing ablations)")
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs)
+    build(force=a.force, jobs=a.jobs, ablation=a.ablation)
     sys.exit(0)

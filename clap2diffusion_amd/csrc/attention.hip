@@ -66,12 +66,19 @@ __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B
 // (one slot per tile, staged once) and the workgroup walks `qpb` consecutive 128-query
 // blocks of its (image, head) over them -- the streaming form re-staged K/V and paid
 // the staging latency once per 128 queries for ~6 MFLOP of work.
-template <int D, bool MASK, bool NEGC, bool RES = false>
+// KBIAS: an additive per-key score bias (attention_mask of the processor API, the
+// key-padding form diffusers builds: fp32 kbias[b * kb_ldb + h * kb_ldh + key], natural-
+// log units, added to q.k * scale before the softmax); only with NEGC = false, where s
+// holds the unscaled q.k, so the bias enters as bias / scale.
+template <int D, bool MASK, bool NEGC, bool RES = false, bool KBIAS = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? ATTN_WPE : 1)))
 attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
-                                                       int kv_div, int nqb, int abl, int qpb = 1) {
+                                                       int kv_div, int nqb, int abl, int qpb = 1,
+                                                       const float* __restrict__ kbias = nullptr, int kb_ldb = 0,
+                                                       int kb_ldh = 0, float kb_mul = 0.f) {
+    static_assert(!(KBIAS && NEGC), "key bias only on the fma-softmax form");
     using C = AttnCfg<D>;
     constexpr int SLOT = C::K_BYTES + C::V_BYTES;
     constexpr int NSLOT = RES ? 2 : 1;
@@ -207,7 +214,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
     for (int t = 0; t < ntiles; ++t) {
-        if (!RES && t + 1 < ntiles && !abl) gload(t + 1);
+        if (!RES && t + 1 < ntiles && !C2D_ABL(abl, 1)) gload(t + 1);
         const char* Kt = Ks + (RES ? t * SLOT : 0);
         const char* Vt = Vs + (RES ? t * SLOT : 0);
 
@@ -247,6 +254,18 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
             for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
                 for (int kg = 0; kg < 4; ++kg) s[qg][kg] += st[qg][kg];
+        }
+        if (KBIAS) {   // additive key bias (lane holds keys 16 kg + 4 g + r of its query)
+            const float* kbr = kbias + (size_t)b * kb_ldb + (size_t)h * kb_ldh;
+#pragma unroll
+            for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = t * 64 + kg * 16 + g * 4 + r;
+                    const float bb = key < lk ? kbr[key] * kb_mul : 0.f;
+                    s[0][kg][r] += bb;
+                    s[1][kg][r] += bb;
+                }
         }
         if (MASK && (t + 1) * 64 > lk) {  // tail tile: mask keys >= lk
 #pragma unroll
@@ -344,7 +363,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
         // immediates) measured no faster at d = 40, 3 % faster at d = 80 and 10 %
         // slower on the 77-key cross-attention: the cost is the gload / swrite
         // instructions, not the second barrier.
-        if (!RES && t + 1 < ntiles && !abl) {
+        if (!RES && t + 1 < ntiles && !C2D_ABL(abl, 1)) {
             __syncthreads();
             swrite(0);
             __syncthreads();
@@ -674,10 +693,14 @@ __global__ void __launch_bounds__(256) attn_pp_kernel(const f16* __restrict__ q,
 // in-flight S tile takes it to 148 VGPR + 24 AGPR = 2 waves/SIMD vs 126 + 40 = 3 for
 // attn_fwd_kernel<40>, and the doubled K/V ring halves the blocks LDS admits, so it is
 // off by default.
-static int attn_abl() {   // C2D_ATTN_ABL=1: timing ablation of the K/V staging (wrong results)
+static int attn_abl() {   // C2D_ATTN_ABL=1: timing ablation of the K/V staging (ablation builds only)
+#ifdef C2D_ENABLE_ABLATION
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_ATTN_ABL"); v = e ? atoi(e) : 0; }
     return v;
+#else
+    return 0;
+#endif
 }
 
 static bool attn_negc() {   // C2D_ATTN_NEGC=0: the fma-per-score softmax (A/B only)
@@ -696,6 +719,33 @@ static int attn_pipelined() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
     return v;
+}
+
+// attention with an additive per-key bias: the fma-softmax kernels (resident K/V for
+// lk <= 128, streaming otherwise); the bias is pre-multiplied by 1 / scale
+template <int D>
+static int launch_attn_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                            int batch, int heads, int lq, int lk, float scale, int kv_div, const float* kbias,
+                            int kb_ldb, int kb_ldh, hipStream_t s) {
+    using C = AttnCfg<D>;
+    const int nqb = (lq + 127) / 128;
+    const int smem = C::K_BYTES + C::V_BYTES;
+    const float sl2 = scale * 1.4426950408889634f, mul = 1.0f / scale;
+    if (lk <= 128) {
+        const long bhs = (long)batch * heads;
+        int qpb = (int)((bhs * nqb) / 1024);
+        qpb = qpb < 1 ? 1 : qpb > nqb ? nqb : qpb;
+        const int ngrp = (nqb + qpb - 1) / qpb;
+        dim3 g2((unsigned)(ngrp * bhs));
+        hipLaunchKernelGGL((attn_fwd_kernel<D, true, false, true, true>), g2, dim3(256), 2 * smem, s, (const f16*)q,
+                           ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, sl2, kv_div, nqb,
+                           0, qpb, kbias, kb_ldb, kb_ldh, mul);
+    } else {
+        hipLaunchKernelGGL((attn_fwd_kernel<D, true, false, false, true>), dim3(nqb * batch * heads), dim3(256), smem,
+                           s, (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk,
+                           sl2, kv_div, nqb, 0, 1, kbias, kb_ldb, kb_ldh, mul);
+    }
+    return check_launch();
 }
 
 template <int D>
@@ -814,6 +864,31 @@ extern "C" int c2d_attention_fwd(const void* q, int ldq, const void* k, int ldk,
         case 160: return launch_attn<160>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, s);
         default: return C2D_E_SHAPE;
     }
+}
+
+extern "C" int c2d_attention_fwd_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                                      void* o, int ldo, int batch, int heads, int lq, int lk, int d, float scale,
+                                      int kv_div, const float* key_bias, int bias_ld_batch, int bias_ld_head,
+                                      void* stream) {
+    if (!key_bias) return c2d_attention_fwd(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, d, scale, kv_div,
+                                            stream);
+    if (!q || !k || !v || !o || kv_div <= 0) return C2D_E_ARG;
+    if (batch <= 0 || heads <= 0 || lq <= 0 || lk <= 0 || scale == 0.f) return C2D_E_SHAPE;
+    if (bias_ld_batch < 0 || bias_ld_head < 0) return C2D_E_SHAPE;
+    if ((ldq & 7) || (ldk & 7) || (ldv & 7) || (ldo & 3)) return C2D_E_ALIGN;
+    if (!aligned16(q) || !aligned16(k) || !aligned16(v) || ((uintptr_t)o & 7)) return C2D_E_ALIGN;
+    if (heads * d > ldq || heads * d > ldk || heads * d > ldv || heads * d > ldo) return C2D_E_SHAPE;
+    hipStream_t s = (hipStream_t)stream;
+#define C2D_ATTN_B(DD) launch_attn_bias<DD>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, \
+                                            key_bias, bias_ld_batch, bias_ld_head, s)
+    switch (d) {
+        case 40: return C2D_ATTN_B(40);
+        case 64: return C2D_ATTN_B(64);
+        case 80: return C2D_ATTN_B(80);
+        case 160: return C2D_ATTN_B(160);
+        default: return C2D_E_SHAPE;
+    }
+#undef C2D_ATTN_B
 }
 
 extern "C" int c2d_window_attention(const void* qkv, int ld_qkv, const int* row_map, int n_windows, int heads, int d,

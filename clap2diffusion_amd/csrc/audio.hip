@@ -1,11 +1,15 @@
-// CLAP log-mel front end for gfx950: the work of transformers' ClapFeatureExtractor
-// (truncation "rand_trunc", padding "repeatpad"; feature_extraction_clap.py
-// _get_input_mel / _np_extract_fbank_features, audio_utils.spectrogram /
-// power_to_db), called by the reference at models/audio_encoder.py:160-170.
+// CLAP log-mel front end for gfx950: the reference's audio composition
+// CLAPAudioEncoder.preprocess_audio (models/audio_encoder.py:121-129: zero-pad to
+// target_length * sample_rate = max_len samples, or keep the first max_len) followed
+// by transformers' ClapFeatureExtractor on that exactly-max_len clip
+// (feature_extraction_clap.py _get_input_mel: neither the repeat-pad nor the random
+// crop fires at exact length; _np_extract_fbank_features, audio_utils.spectrogram /
+// power_to_db), called by the reference at models/audio_encoder.py:163-171.
 //
 // One 256-thread workgroup per (clip, frame):
-//   1. gather the frame's 1024 samples: repeat-pad of the clip to max_len (np.tile
-//      n_repeat = max_len // n times, zero tail), then the centre reflect pad of
+//   1. gather the frame's 1024 samples: the clip zero-padded / truncated to max_len
+//      (lengths are clamped to [0, max_len], so a longer clip keeps its first max_len
+//      samples and an empty one reads as silence), then the centre reflect pad of
 //      n_fft/2 (np.pad mode "reflect"), times the periodic Hann window;
 //   2. 1024-point complex FFT in LDS, radix-2 Stockham (natural-order output, fp32,
 //      twiddles from sincospi) -- fp32 keeps bins ~120 dB below the frame peak exact,
@@ -33,17 +37,15 @@ __global__ void __launch_bounds__(256) clap_log_mel_kernel(const float* __restri
     const int tid = threadIdx.x;
     const int fr = blockIdx.x % frames, bi = blockIdx.x / frames;
     const float* x = wave + offsets[bi];
-    const int n = lengths[bi];
-    const int reps = max_len / n;          // np.tile count of repeatpad (1 when n == max_len)
-    const int rep_len = reps * n;
+    const int n = min(max(lengths[bi], 0), max_len);   // zero-pad / truncate (audio_encoder.py:123-129)
 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const int i = tid + 256 * r;
-        int p = fr * hop + i - MEL_NFFT / 2;   // position in the repeat-padded clip
+        int p = fr * hop + i - MEL_NFFT / 2;   // position in the zero-padded clip
         if (p < 0) p = -p;                     // reflect (edge sample not repeated)
         if (p >= max_len) p = 2 * (max_len - 1) - p;
-        const float s = p < rep_len ? x[p % n] : 0.f;
+        const float s = p < n ? x[p] : 0.f;
         buf[0][i] = make_float2(s * window[i], 0.f);
     }
     __syncthreads();

@@ -556,7 +556,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         asm volatile("" ::: "memory");
         // p.abl (timing ablation only, C2D_GEMM_ABL): bit 0 skips the DMA after the
         // prologue stages, bit 1 skips the MFMAs (fragments still read and kept live)
-        if (kt + STAGES - 1 < ke && !(p.abl & 1)) issue(kt + STAGES - 1, wr);
+        if (kt + STAGES - 1 < ke && !(C2D_ABL(p.abl, 1))) issue(kt + STAGES - 1, wr);
         const char* S = smem + rd * STAGE;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
             for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + fb0[kk] + t * 2048);
 #pragma unroll
             for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + fa0[kk] + t * 2048);
-            if (p.abl & 2) {
+            if (C2D_ABL(p.abl, 2)) {
 #pragma unroll
                 for (int t = 0; t < TN; ++t) asm volatile("" :: "v"(fb[t]));
 #pragma unroll
@@ -665,7 +665,12 @@ namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
 static void launch_dma(const IgemmParams& p, hipStream_t s) {
-    constexpr int smem = STAGES * (WM * TM + WN * TN) * 16 * 128;
+    // the ring, or the fp32 epilogue image (per wave 16 * min(TM, 2) rows x (TN * 16 + 4)
+    // floats) that reuses it after the main loop, whichever is larger
+    constexpr int ring = STAGES * (WM * TM + WN * TN) * 16 * 128;
+    constexpr int epi = WM * WN * 16 * (TM < 2 ? TM : 2) * (TN * 16 + 4) * 4;
+    constexpr int smem = ring > epi ? ring : epi;
+    static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     auto k = igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>;
     static bool attr = false;
     if (!attr) {
@@ -699,11 +704,12 @@ static int gemm_mode() {
     return v;
 }
 
-// C2D_GEMM_TILE=k forces DMA tile config k (shape sweeps); 0 = heuristic.
+// C2D_GEMM_TILE=k forces DMA tile config k (shape sweeps, the per-tile parity test);
+// 0 = heuristic.  Read per call (not cached) so a test can walk every tile id in one
+// process; the cost is one getenv per launch, outside any captured graph's replay.
 static int gemm_tile() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GEMM_TILE"); v = e ? atoi(e) : 0; }
-    return v;
+    const char* e = getenv("C2D_GEMM_TILE");
+    return e ? atoi(e) : 0;
 }
 
 template <int WM, int WN, int TM, int TN, int ST>
@@ -723,17 +729,11 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 // has an odd per-wave column-tile count, so GEGLU skips it; GEGLU never splits.
 struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
 static const DmaTile kDmaTiles[] = {
-    // 32x32x16 MFMA, deep LDS-DMA ring (igemm_m32.h); rate 0 = only when forced (C2D_GEMM_TILE)
-    {20, 256, 320, 1, 0.0f, true},
-    {23, 256, 320, 1, 0.0f, true},
-    {21, 256, 320, 1, 0.0f, true},
-    {24, 256, 320, 1, 0.0f, true},
-    {26, 128, 320, 1, 0.0f, true},
+    // 32x32x16 MFMA, LDS-DMA ring (igemm_m32.h); rate 0 = chosen by the rules in plan_for only
     {25, 256, 320, 1, 0.0f, true},
     {28, 256, 256, 1, 0.0f, true},
     {29, 256, 128, 1, 0.0f, true},
-    {22, 256, 320, 1, 0.0f, true},
-    {30, 256, 320, 1, 0.0f, true},
+    // 16x16x32 MFMA LDS-DMA family, costed by plan_dma
     {7, 128, 320, 1, 3.1f, false},
     {1, 256, 128, 1, 2.9f, true},
     {2, 128, 128, 1, 2.2f, true},
@@ -767,11 +767,15 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
 }
 
 // C2D_GEMM_ABL: timing ablation of the DMA kernels (1 = no DMA, 2 = no MFMA; m32: 4 = no epilogue,
-// 8 = with 2, no fragment reads either); wrong results by design
+// 8 = with 2, no fragment reads either); wrong results by design, so only in -DC2D_ENABLE_ABLATION builds
 static int gemm_abl() {
+#ifdef C2D_ENABLE_ABLATION
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_GEMM_ABL"); v = e ? atoi(e) : 0; }
     return v;
+#else
+    return 0;   // production build: no ablation (common.h C2D_ABL)
+#endif
 }
 
 // K-step order of the 3x3 DMA kernels.  1 (default): for each 64-channel block all
@@ -804,9 +808,8 @@ static bool epi_direct_ok(const c2d_conv_desc* d) {
 
 // C2D_GEMM_SPLIT=s forces s K slices (when the workspace allows); 0 = model
 static int gemm_split() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GEMM_SPLIT"); v = e ? atoi(e) : 0; }
-    return v;
+    const char* e = getenv("C2D_GEMM_SPLIT");
+    return e ? atoi(e) : 0;
 }
 
 // Tile choice.  Measured on gfx950 over the UNet's conv / linear shapes
@@ -850,16 +853,9 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
     switch (pl.id) {
-        case 20: return run_m32<4, 2, 2, 5, 32, 4, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 32
-        case 23: return run_m32<4, 2, 2, 5, 64, 2, false>(p, ksize, cout, s);  // 256x320, 8 waves of 64x160, BK 64
-        case 21: return run_m32<4, 2, 2, 5, 32, 4, 2>(p, ksize, cout, s);      // as 20, DMA interleaved with MFMAs
-        case 24: return run_m32<4, 2, 2, 5, 64, 2, 2>(p, ksize, cout, s);      // as 23, DMA interleaved with MFMAs
-        case 25: return run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s);   // as 24, fragments double-buffered
-        case 22: return run_m32<4, 2, 2, 5, 32, 4, 3>(p, ksize, cout, s);      // as 21, fragments double-buffered
+        case 25: return run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s);   // 256x320, 8 waves of 64x160
         case 28: return run_m32<4, 2, 2, 4, 64, 2, 3>(p, ksize, cout, s);      // 256x256, 8 waves of 64x128
         case 29: return run_m32<4, 2, 2, 2, 64, 3, 3>(p, ksize, cout, s);      // 256x128, 8 waves of 64x64, 3 stages
-        case 26: return run_m32<4, 2, 1, 5, 32, 5, 2>(p, ksize, cout, s);      // 128x320, 8 waves of 32x160, BK 32
-        case 30: return run_pp<4, 2, 2, 5>(p, ksize, cout, s);   // 256x320 ping-pong, 8 waves of 64x160
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
         case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64
         case 2: return run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s);   // 128x128, 4 waves of 64x64
@@ -883,6 +879,25 @@ extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     const long M = (long)d->n * d->oh * d->ow;
     const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act);
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
+}
+
+extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit) {
+    if (!d || !tile_id || !ksplit) return C2D_E_ARG;
+    if (d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return C2D_E_SHAPE;
+    if (!dma_eligible(d)) {
+        *tile_id = 0;
+        *ksplit = 1;
+        return C2D_OK;
+    }
+    const long M = (long)d->n * d->oh * d->ow;
+    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act);
+    if (pl.split > 1) {
+        const size_t need = (size_t)pl.split * M * d->cout * sizeof(float);
+        if (!(d->ws && d->ws_bytes >= need && aligned16(d->ws))) pl.split = 1;
+    }
+    *tile_id = pl.id;
+    *ksplit = pl.split;
+    return C2D_OK;
 }
 
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {

@@ -349,10 +349,10 @@ igemm_m32_kernel(IgemmParams p) {
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        const bool do_issue = kt + STAGES - 1 < ke && !(p.abl & 1);
+        const bool do_issue = kt + STAGES - 1 < ke && !(C2D_ABL(p.abl, 1));
         if (DB < 2 && do_issue) ld.issue(p, kt + STAGES - 1, smem + wr * STAGE, wave);
         const char* S = smem + rd * STAGE;
-        if (DB >= 2 && !(p.abl & 2)) {
+        if (DB >= 2 && !(C2D_ABL(p.abl, 2))) {
             constexpr int NSLOT = NS * TM * TN, P = Loader::PMAX;
             // with one stage in flight the pieces must land within this step: keep
             // them in its first two thirds
@@ -390,9 +390,9 @@ igemm_m32_kernel(IgemmParams p) {
                 __builtin_amdgcn_s_setprio(0);
             }
             if (do_issue) ld.advance();
-        } else if (p.abl & 2) {   // timing ablation: fragments read and kept live, no MFMA
+        } else if (C2D_ABL(p.abl, 2)) {   // timing ablation: fragments read and kept live, no MFMA
 #pragma unroll
-            for (int s = 0; s < NS && !(p.abl & 8); ++s) {
+            for (int s = 0; s < NS && !(C2D_ABL(p.abl, 8)); ++s) {
 #pragma unroll
                 for (int t = 0; t < TN; ++t)
                     asm volatile("" :: "v"(*reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo[s])));
@@ -446,7 +446,7 @@ igemm_m32_kernel(IgemmParams p) {
         wr = (wr + 1 == STAGES) ? 0 : wr + 1;
     }
     const int mw0 = m0 + wm * TM * 32, nw0 = n0 + wn * TN * 32;
-    if (p.abl & 4) {   // timing ablation: no epilogue (the accumulators kept live)
+    if (C2D_ABL(p.abl, 4)) {   // timing ablation: no epilogue (the accumulators kept live)
         float z = 0.f;
 #pragma unroll
         for (int a = 0; a < TN; ++a)
@@ -479,10 +479,24 @@ igemm_m32_kernel(IgemmParams p) {
     epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
 }
 
+// Dynamic LDS of a 32x32-family launch: the DMA ring, and the fp32 epilogue image
+// epilogue32_lds writes into the same allocation after the main loop (per wave 32
+// rows x (min(TN,3)*32 + 4) floats).  Sizing by the ring alone let a small ring (the
+// 2-stage BK-32 variant of round 1: 72 KiB ring vs 100 KiB image at 256x320) have its
+// epilogue write past the allocation -- the root cause of that variant's wrong results.
+template <int NW, int TN>
+constexpr int m32_epi_bytes() { return NW * 32 * ((TN < 3 ? TN : 3) * 32 + 4) * 4; }
+template <int WM, int WN, int TM, int TN, int BK, int STAGES>
+constexpr int m32_smem_bytes() {
+    constexpr int ring = STAGES * (WM * TM + WN * TN) * 32 * 2 * BK;
+    constexpr int epi = m32_epi_bytes<WM * WN, TN>();
+    return ring > epi ? ring : epi;
+}
+
 template <int WM, int WN, int TM, int TN, int BK, int STAGES, int KS, int DB, int WPE, int EACT>
 static void launch_m32(const IgemmParams& p, hipStream_t s) {
-    constexpr int smem = STAGES * (WM * TM + WN * TN) * 32 * 2 * BK;
-    static_assert(smem <= 160 * 1024, "LDS ring too large");
+    constexpr int smem = m32_smem_bytes<WM, WN, TM, TN, BK, STAGES>();
+    static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE, EACT>;
     static bool attr = false;
     if (!attr) {
@@ -519,179 +533,6 @@ static void run_m32(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     p.nkt *= 64 / BK;   // the planner counts 64-deep K steps
     if (ksize == 1) launch_m32_act<WM, WN, TM, TN, BK, ST, DB, 1, WPE, DIRECT>(p, s);
     else launch_m32_act<WM, WN, TM, TN, BK, ST, DB, 3, WPE, DIRECT>(p, s);
-}
-
-// ---------------------------------------------------------------------------
-// Ping-pong implicit GEMM (32x32x16 MFMA, BK = 32, 4-stage LDS-DMA ring).
-//
-// The 8 waves form two groups (waves 0-3, 4-7: one wave of each per SIMD).
-// Group 1 runs one barrier behind group 0, so between two consecutive
-// workgroup barriers one group issues its MFMA cluster while the other issues
-// its LDS fragment reads (and DMA): the SIMD's matrix pipe alternates between
-// the two waves it hosts instead of idling while both read LDS.  Fragments are
-// single-buffered (the overlap is across the two waves of a SIMD, not inside a
-// wave), which keeps the 160 accumulator registers of a 64x160 wave tile
-// spill-free.
-//
-// A phase = one 16-deep k sub-step (TM*TN MFMAs), two per K step kt:
-//   phase (kt,0): read frags (kt,0);                                   B1; MFMA; B2
-//   phase (kt,1): DMA stage kt+3; read frags (kt,1); wait stage kt+1;   B1; MFMA; B2
-// Hazards, with the one-barrier stagger between the groups:
-//   RAW  stage kt+1 is first read in phase (kt+1,0), after this wave's B2 of
-//        (kt,1); every wave waited for its own pieces of stage kt+1 before its
-//        B1 of (kt,1), which for the other group is at most that barrier.
-//   WAR  the DMA of stage kt+3 (phase (kt,1), after this wave's B2 of (kt,0))
-//        overwrites the slot of stage kt-1, whose last fragments every wave
-//        consumed (lgkmcnt) before its B2 of (kt-1,1): at least one global
-//        barrier earlier for either group.
-template <int WM, int WN, int TM, int TN, int KS>
-__global__ void __launch_bounds__(64 * WM * WN) igemm_pp_kernel(IgemmParams p) {
-    constexpr int BK = 32, STAGES = 4;
-    constexpr int NW = WM * WN;
-    static_assert(NW == 8, "two groups of four waves");
-    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-    constexpr int RB = 2 * BK, STAGE = (BM + BN) * RB;
-    typedef M32Loader<BM, BN, BK, NW, KS> Loader;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2;
-    const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-    const int bid = xcd_remap(blockIdx.x, p.gx * p.gy * p.ksplit);
-    const int tile = bid / p.ksplit, slice = bid - tile * p.ksplit;
-    const int mt = tile / p.gx, nt = tile - mt * p.gx;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int nk_all = p.kpad / BK;
-    const int kb = slice * p.nkt, ke = min(nk_all, kb + p.nkt);
-    const int per = Loader::pieces(wave);
-
-    Loader ld;
-    ld.init(p, m0, n0, wave, lane, kb);
-
-    const int fo0 = lds_sw<BK>(lane & 31, lane >> 5), fo1 = lds_sw<BK>(lane & 31, 2 + (lane >> 5));
-    const int a_base = wm * TM * 32 * RB, b_base = BM * RB + wn * TN * 32 * RB;
-
-    f32x16 acc[TN][TM];
-#pragma unroll
-    for (int a = 0; a < TN; ++a)
-#pragma unroll
-        for (int b = 0; b < TM; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-#define C2D_BAR() do { asm volatile("" ::: "memory"); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } while (0)
-    f16x8 fa[TM], fb[TN];
-    auto rd_frags = [&](int stage, int fo) {
-        if (p.abl & 4) return;   // timing ablation: no fragment reads
-        const char* S = smem + (stage & (STAGES - 1)) * STAGE;
-#pragma unroll
-        for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 32 * RB + fo);
-#pragma unroll
-        for (int t = 0; t < TM; ++t) fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + t * 32 * RB + fo);
-    };
-    auto mfma = [&]() {
-        if (p.abl & 2) {   // timing ablation: fragments kept live, no MFMA
-#pragma unroll
-            for (int t = 0; t < TM; ++t) asm volatile("" :: "v"(fa[t]));
-#pragma unroll
-            for (int t = 0; t < TN; ++t) asm volatile("" :: "v"(fb[t]));
-            return;
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int b = 0; b < TM; ++b)
-#pragma unroll
-            for (int a = 0; a < TN; ++a)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[a], fa[b], acc[a][b], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-    };
-    // vmcnt(per * n) for n = 0, 1, 2 younger stages of this wave in flight
-    auto wait_younger = [&](int n) {
-        if (n >= 2) {
-            if (per == Loader::PMAX) wait_vm_c<2 * Loader::PMAX>();
-            else wait_vm_c<2 * Loader::PMIN>();
-        } else if (n == 1) {
-            if (per == Loader::PMAX) wait_vm_c<Loader::PMAX>();
-            else wait_vm_c<Loader::PMIN>();
-        } else {
-            wait_vm_c<0>();
-        }
-    };
-
-    // prologue: stages kb..kb+2 in flight, stage kb landed everywhere before the first read
-#pragma unroll
-    for (int s0 = 0; s0 < STAGES - 1; ++s0)
-        if (kb + s0 < ke) ld.issue(p, kb + s0, smem + ((kb + s0) & (STAGES - 1)) * STAGE, wave);
-    wait_younger(min(2, ke - 1 - kb));
-    C2D_BAR();
-    if (grp) C2D_BAR();   // group 1 runs one barrier behind
-
-    for (int kt = kb; kt < ke; ++kt) {
-        // ---- phase (kt, 0)
-        rd_frags(kt, fo0);
-        C2D_BAR();
-        mfma();
-        C2D_BAR();
-        // ---- phase (kt, 1)
-        if (kt + STAGES - 1 < ke && !(p.abl & 1))
-            ld.issue(p, kt + STAGES - 1, smem + ((kt + STAGES - 1) & (STAGES - 1)) * STAGE, wave);
-        rd_frags(kt, fo1);
-        if (kt + 1 < ke) wait_younger((kt + 2 < ke) + (kt + 3 < ke));   // stage kt+1 landed
-        C2D_BAR();
-        mfma();
-        C2D_BAR();
-    }
-    if (!grp) C2D_BAR();  // balance the stagger before the workgroup ends
-#undef C2D_BAR
-
-    const int mw0 = m0 + wm * TM * 32, nw0 = n0 + wn * TN * 32;
-    if (p.ksplit > 1) {
-        float* dst = p.ws + (size_t)slice * p.M * p.cout;
-#pragma unroll
-        for (int b = 0; b < TM; ++b) {
-            const int m = mw0 + b * 32 + (lane & 31);
-#pragma unroll
-            for (int a = 0; a < TN; ++a)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int j = nw0 + a * 32 + g * 8 + 4 * (lane >> 5);
-                    f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
-                    if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = v;
-                }
-        }
-        return;
-    }
-    __syncthreads();   // every wave is done reading the staging ring
-    epilogue32_lds<TM, TN>(p, acc, mw0, nw0, lane, wave, smem);
-}
-
-template <int WM, int WN, int TM, int TN, int KS>
-static void launch_pp(const IgemmParams& p, hipStream_t s) {
-    constexpr int smem = 4 * (WM * TM + WN * TN) * 32 * 64;
-    static_assert(smem <= 160 * 1024, "LDS ring too large");
-    auto k = igemm_pp_kernel<WM, WN, TM, TN, KS>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr = true;
-    }
-    hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
-    if (p.ksplit > 1) {
-        const size_t total = (size_t)p.M * (p.cout >> 2);
-        const size_t want = (total + 255) / 256;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
-    }
-}
-
-template <int WM, int WN, int TM, int TN>
-static void run_pp(IgemmParams& p, int ksize, int cout, hipStream_t s) {
-    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-    p.gx = (cout + BN - 1) / BN;
-    p.gy = (p.M + BM - 1) / BM;
-    p.nkt *= 2;   // the planner counts 64-deep K steps
-    if (ksize == 1) launch_pp<WM, WN, TM, TN, 1>(p, s);
-    else launch_pp<WM, WN, TM, TN, 3>(p, s);
 }
 
 }  // namespace c2d

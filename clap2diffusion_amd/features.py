@@ -1,14 +1,15 @@
 """CLAP log-mel front end on the GPU (c2d_clap_log_mel).
 
-Does the work the reference hands to transformers' ClapProcessor /
-ClapFeatureExtractor (models/audio_encoder.py:163-167, truncation "rand_trunc",
-padding "repeatpad"): waveforms in, [B, 1001, 64] fp32 dB log-mel features out,
-on device, ready for the HTSAT tower.  The host keeps only what is host work in
-the extractor too: the random crop of clips longer than max_length
-(np.random.randint, feature_extraction_clap.py _get_input_mel) and the constant
-tables (periodic Hann window, Slaney mel filter bank of audio_utils.mel_filter_bank)
-built once at construction.  The STFT, power, mel projection and dB run in one
-HIP kernel; there is no CPU fallback.
+Does the work of the reference's audio composition: CLAPAudioEncoder.preprocess_audio
+(models/audio_encoder.py:121-129: zero-pad a clip to target_length x sample_rate =
+480,000 samples, or keep its first 480,000) followed by transformers' ClapProcessor /
+ClapFeatureExtractor on that exact-length clip (models/audio_encoder.py:163-167; at
+exact length the extractor's repeat-pad and random crop never fire).  Waveforms in,
+[B, 1001, 64] fp32 dB log-mel features out, on device, ready for the HTSAT tower.
+The host only truncates (a view, no copy) and builds the constant tables once
+(periodic Hann window, Slaney mel filter bank of audio_utils.mel_filter_bank); the
+zero padding, STFT, power, mel projection and dB run in one HIP kernel; there is no
+CPU fallback.
 """
 from __future__ import annotations
 
@@ -47,7 +48,7 @@ def slaney_mel_filters(n_bins: int, n_mels: int, fmin: float, fmax: float, sr: i
 
 
 class ClapLogMel:
-    """Device-side ClapFeatureExtractor(truncation="rand_trunc", padding="repeatpad")."""
+    """Device-side preprocess_audio (zero-pad / truncate to max_length_s) + ClapFeatureExtractor."""
 
     def __init__(self, device, feature_size: int = 64, sampling_rate: int = 48_000, hop_length: int = 480,
                  max_length_s: int = 10, fft_window_size: int = 1024, frequency_min: float = 0.0,
@@ -67,16 +68,18 @@ class ClapLogMel:
         self.filter_range = torch.from_numpy(rng).to(self.device)
 
     def crop(self, audios: list) -> list:
-        """Host part of _get_input_mel: random crop of clips longer than max_length."""
+        """Host part of preprocess_audio (models/audio_encoder.py:109-129): mono (channel
+        mean of a [samples, channels] array) and the first max_len samples of a longer
+        clip; shorter clips are zero-padded by the kernel (lengths < max_len)."""
         out = []
         for a in audios:
-            a = np.asarray(a, dtype=np.float32).reshape(-1)
+            a = np.asarray(a, dtype=np.float32)
+            if a.ndim > 1:
+                a = a.mean(axis=-1)
+            a = a.reshape(-1)
             if a.size == 0:
                 raise ValueError("empty waveform")
-            if a.size > self.max_len:
-                idx = np.random.randint(0, a.size - self.max_len + 1)
-                a = a[idx: idx + self.max_len]
-            out.append(a)
+            out.append(a[: self.max_len])
         return out
 
     def __call__(self, audios: list, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -89,8 +92,9 @@ class ClapLogMel:
 
     def from_device(self, wave: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
                     out: torch.Tensor | None = None) -> torch.Tensor:
-        """wave fp32 (clips concatenated, already cropped), offsets int64 [B], lengths int32 [B],
-        all on device -> features fp32 [B, frames, n_mels]."""
+        """wave fp32 (clips concatenated), offsets int64 [B], lengths int32 [B], all on device
+        -> features fp32 [B, frames, n_mels].  The kernel clamps each length to [0, max_len]:
+        a longer clip keeps its first max_len samples, a shorter one is zero-padded."""
         b = offsets.numel()
         assert wave.dtype == torch.float32 and offsets.dtype == torch.int64 and lengths.dtype == torch.int32
         if out is None:

@@ -131,8 +131,31 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
     if wsb:
         ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
         d.ws = ptr(ws); d.ws_bytes = wsb
+    if _plan_probe is not None:
+        tid, ks = ctypes.c_int(), ctypes.c_int()
+        check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
+        _plan_probe.append((tid.value, ks.value))
     check(lib().c2d_conv2d_igemm(ctypes.byref(d), stream_ptr()), "c2d_conv2d_igemm")
     return out
+
+
+_plan_probe: list | None = None
+
+
+class record_conv_plans:
+    """Context manager collecting the (tile_id, ksplit) plan of every ops.conv call
+    (c2d_conv2d_igemm_plan) -- lets tests assert which kernel configuration ran."""
+
+    def __enter__(self):
+        global _plan_probe
+        self.plans = []
+        _plan_probe = self.plans
+        return self.plans
+
+    def __exit__(self, *exc):
+        global _plan_probe
+        _plan_probe = None
+        return False
 
 
 def group_norm_stats(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor,
@@ -208,16 +231,31 @@ def layer_norm(x2d: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: 
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, heads: int, lq: int, lk: int,
-              d: int, scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """q/k/v: 2-D row views [batch*L, >= heads*d] (column slices allowed)."""
+              d: int, scale: float | None = None, out: torch.Tensor | None = None,
+              key_bias: torch.Tensor | None = None) -> torch.Tensor:
+    """q/k/v: 2-D row views [batch*L, >= heads*d] (column slices allowed).
+    key_bias: optional additive per-key score bias, fp32 [batch or 1, heads or 1, lk]
+    (c2d_attention_fwd_bias; size-1 dims broadcast)."""
     _require(q, "q")
     if scale is None:
         scale = 1.0 / math.sqrt(d)
     if out is None:
         out = torch.empty((batch * lq, heads * d), device=q.device, dtype=F16)
-    rc = lib().c2d_attention_fwd(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-                                 out.stride(0), batch, heads, lq, lk, d, float(scale), 1, stream_ptr())
-    check(rc, "c2d_attention_fwd")
+    if key_bias is None:
+        rc = lib().c2d_attention_fwd(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+                                     out.stride(0), batch, heads, lq, lk, d, float(scale), 1, stream_ptr())
+        check(rc, "c2d_attention_fwd")
+        return out
+    kb = key_bias.to(device=q.device, dtype=torch.float32)
+    if kb.dim() != 3 or kb.shape[-1] != lk or kb.shape[0] not in (1, batch) or kb.shape[1] not in (1, heads):
+        raise ValueError(f"key_bias must be [batch|1, heads|1, {lk}], got {tuple(kb.shape)}")
+    kb = kb.contiguous()
+    ldb = kb.stride(0) if kb.shape[0] > 1 else 0
+    ldh = kb.stride(1) if kb.shape[1] > 1 else 0
+    rc = lib().c2d_attention_fwd_bias(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+                                      out.stride(0), batch, heads, lq, lk, d, float(scale), 1, ptr(kb), ldb, ldh,
+                                      stream_ptr())
+    check(rc, "c2d_attention_fwd_bias")
     return out
 
 

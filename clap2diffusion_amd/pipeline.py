@@ -12,8 +12,9 @@ runs the real path:
 Composition contract (SURVEY.md §8(a)): ehs = CLIP([uncond "", prompt]);
 routed tokens repeated for both CFG halves; adapter + Norm-60 and the legacy
 HierarchicalAudioV4 outputs are computed for API fidelity but not fed to the UNet.
-Checkpoints are loaded when present (audio_projector_stage2.pth 'adapter_state_dict',
-hierarchical_v4_final.pth), otherwise every network uses seeded synthetic weights.
+Checkpoints are loaded when present (clap_encoder.pth -> the HTSAT tower,
+audio_projector_stage2.pth 'adapter_state_dict', hierarchical_v4_final.pth; all with
+weights_only=True), otherwise every network uses seeded synthetic weights.
 """
 from __future__ import annotations
 
@@ -52,6 +53,13 @@ def synthetic_thunder(seed: int = 0, seconds: float = 10.0, sr: int = SR) -> np.
     return (y / (np.abs(y).max() + 1e-8)).astype(np.float32)
 
 
+def initial_latents(seeds: list[int], h: int, w: int, device=None) -> torch.Tensor:
+    """Per-sample CPU generator (torch.Generator().manual_seed(seed) -> randn [4, h, w]):
+    identical latents on any number of GPUs."""
+    lat = [torch.randn(4, h, w, generator=torch.Generator().manual_seed(int(s))) for s in seeds]
+    return torch.stack(lat).to(device)
+
+
 def _read_wav(path: str) -> tuple[np.ndarray, int]:
     with wave.open(str(path), "rb") as f:
         sr, ch, sw, n = f.getframerate(), f.getnchannels(), f.getsampwidth(), f.getnframes()
@@ -77,6 +85,7 @@ class AudioToImageInference:
         self.load_models()
         self.OPTIMAL_NORM = 60.0
         self._denoisers = {}
+        self.last_denoiser = None
 
     # ------------------------------------------------------------ models
     def _log(self, *a):
@@ -94,7 +103,13 @@ class AudioToImageInference:
             p.load_state_dict(W.synth_processor_weights(level, self.seed))
             p.to(dev).eval()
         self.clap = HTSATEncoder().to(dev)
-        self.clap.load_clap_state_dict(W.synth_htsat(self.seed))
+        clap_path = self.checkpoint_dir / "clap_encoder.pth"   # reference scripts/inference.py:38-41
+        if clap_path.exists():
+            self._log(f"Loading CLAP encoder from {clap_path}")
+            self.clap.load_clap_state_dict(W.clap_audio_state_dict(
+                torch.load(clap_path, map_location="cpu", weights_only=True)))
+        else:
+            self.clap.load_clap_state_dict(W.synth_htsat(self.seed))
         self.hier_encoder = W.fill_module(ImprovedHierarchicalAudioEncoder(), "improved.", self.seed).to(dev).eval()
         adapter_path = self.checkpoint_dir / "audio_projector_stage2.pth"
         self.audio_adapter = W.fill_module(AudioAdapter(), "adapter.", self.seed).to(dev).eval()
@@ -108,7 +123,7 @@ class AudioToImageInference:
         if hpath.exists():
             self._log(f"Loading Hierarchical Model from {hpath}")
             self.hierarchical_model.load_state_dict(torch.load(hpath, map_location=dev, weights_only=True))
-        self.text_encoder = TextEncoder(dev, seed=self.seed)
+        self.text_encoder = TextEncoder(dev, seed=self.seed)   # CLIPTextModel-keyed seeded weights
         self.vae = VAEDecoder().to(dev)
         self.vae.load_diffusers_state_dict(W.synth_vae_decoder(self.seed))
         self.scheduler = DDIMScheduler()
@@ -164,19 +179,19 @@ class AudioToImageInference:
     # ------------------------------------------------------------ batched core
     def initial_latents(self, seeds: list[int]) -> torch.Tensor:
         """Per-sample CPU generator (seed) -> identical latents on any number of GPUs."""
-        h, w = self.height // 8, self.width // 8
-        lat = [torch.randn(4, h, w, generator=torch.Generator().manual_seed(int(s))) for s in seeds]
-        return torch.stack(lat).to(self.device)
+        return initial_latents(seeds, self.height // 8, self.width // 8, self.device)
 
-    def denoiser(self, b: int, steps: int, guidance: float, ehs, audio_kwargs) -> GraphDenoiser:
-        key = (b, steps, float(guidance))
+    def denoiser(self, b: int, steps: int, guidance: float, ehs, audio_kwargs, latent_hw=None) -> GraphDenoiser:
+        """The captured-graph denoise loop for (batch, steps, guidance, latent size), built once."""
+        h, w = latent_hw or (self.height // 8, self.width // 8)
+        key = (b, steps, float(guidance), h, w)
         d = self._denoisers.get(key)
         if d is None:
             sch = DDIMScheduler()
             sch.set_timesteps(steps)
-            d = GraphDenoiser(self.unet, sch, b, self.height // 8, self.width // 8, guidance, ehs, audio_kwargs,
-                              use_graph=self.use_graph)
+            d = GraphDenoiser(self.unet, sch, b, h, w, guidance, ehs, audio_kwargs, use_graph=self.use_graph)
             self._denoisers[key] = d
+        self.last_denoiser = d
         return d
 
     @torch.no_grad()
@@ -200,14 +215,15 @@ class AudioToImageInference:
     def generate_batch(self, mel: torch.Tensor, prompts: list[str] | None, num_inference_steps: int = 50,
                        guidance_scale: float = 7.5, seeds: list[int] | None = None, use_hierarchical: bool = True,
                        ids: tuple | None = None, latents: torch.Tensor | None = None) -> torch.Tensor:
-        """mel [B, 1001, 64] on device -> uint8 images NHWC [B, H, W, 3] on device."""
+        """mel [B, 1001, 64] on device -> uint8 images NHWC [B, H, W, 3] on device.  The
+        image size follows the latents ([B, 4, H/8, W/8]; default: the pipeline's size)."""
         b = mel.shape[0]
         if ids is None:
             ids = (tokenize([""] * b, self.device), tokenize(prompts or [""] * b, self.device))
         ehs, kw, _ = self.condition(mel, ids[0], ids[1], use_hierarchical)
         if latents is None:
             latents = self.initial_latents(seeds if seeds is not None else list(range(b)))
-        den = self.denoiser(b, num_inference_steps, guidance_scale, ehs, kw)
+        den = self.denoiser(b, num_inference_steps, guidance_scale, ehs, kw, latent_hw=tuple(latents.shape[-2:]))
         den.ehs.copy_(ehs)
         for k, v in kw["audio"].items():
             den.kw["audio"][k].copy_(v)

@@ -34,6 +34,36 @@ def _as_tokens(x: torch.Tensor) -> torch.Tensor:
     return x if x.is_contiguous() else x.contiguous()
 
 
+def key_bias_of(attention_mask: Optional[torch.Tensor], batch: int, heads: int, lk: int) -> Optional[torch.Tensor]:
+    """attention_mask (additive, as Attention.get_attention_scores adds it to q k^T * scale:
+    reference :129) -> the per-key bias c2d_attention_fwd_bias takes, fp32 [B|1, H|1, lk].
+    Accepted: the key-padding forms -- [lk], [1, lk], [B*H | B | 1, 1, lk] (diffusers'
+    prepare_attention_mask output, or the UNet's encoder_attention_mask bias) and
+    [B | 1, 1, 1, lk].  A mask that varies over queries is rejected: the SD1.5 path never
+    builds one and the flash kernel carries a per-key bias only."""
+    if attention_mask is None:
+        return None
+    m = attention_mask
+    if m.shape[-1] != lk:
+        raise ValueError(f"attention_mask last dim {m.shape[-1]} != number of keys {lk}")
+    if m.dim() == 4 and m.shape[1] == 1 and m.shape[2] == 1:
+        m = m[:, 0]
+    if m.dim() == 1:
+        m = m.view(1, 1, lk)
+    elif m.dim() == 2:
+        if m.shape[0] != 1:
+            raise NotImplementedError("2-D attention_mask must be [1, lk] (per-key)")
+        m = m.view(1, 1, lk)
+    if m.dim() != 3 or m.shape[1] != 1:
+        raise NotImplementedError("attention_mask varying over queries is not supported (per-key masks only)")
+    x = m.shape[0]
+    if x == batch * heads and heads > 1:
+        return m.reshape(batch, heads, lk).float()
+    if x in (batch, 1):
+        return m.reshape(x, 1, lk).float()
+    raise ValueError(f"attention_mask batch dim {x} matches neither B*heads={batch * heads}, B={batch} nor 1")
+
+
 class AttnProcessor(nn.Module):
     """Default processor (stock diffusers AttnProcessor semantics) on HIP.
     Self-attention uses the fused [to_q; to_k; to_v] weight of the layer."""
@@ -42,8 +72,6 @@ class AttnProcessor(nn.Module):
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
                  scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
-        if attention_mask is not None:
-            raise NotImplementedError("attention_mask is not used by the SD1.5 sampling path")
         x = _as_tokens(hidden_states)
         b, l, c = x.shape
         x2 = x.view(b * l, c)
@@ -53,7 +81,8 @@ class AttnProcessor(nn.Module):
             qkv = ops.conv(x2, attn.w_qkv, attn.kpad_q, 3 * inner, ksize=1)
             if scale != 1.0:
                 qkv[:, :inner].mul_(scale)
-            o = ops.attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], b, heads, l, l, d)
+            o = ops.attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], b, heads, l, l, d,
+                              key_bias=key_bias_of(attention_mask, b, heads, l))
         else:
             cache = cross_attention_kwargs.get("context_kv")
             kv = cache.get(attn) if cache is not None else None
@@ -63,7 +92,8 @@ class AttnProcessor(nn.Module):
             q = ops.conv(x2, attn.to_q.weight, attn.kpad_q, inner, ksize=1)
             if scale != 1.0:
                 q.mul_(scale)
-            o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d)
+            o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d,
+                              key_bias=key_bias_of(attention_mask, b, heads, lk))
         out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
                              out=None if _residual is None else _residual.reshape(b * l, c))
         return out.view(b, l, c)
@@ -160,15 +190,13 @@ class AudioAttnProcessor(nn.Module):
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
                  scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
-        if attention_mask is not None:
-            raise NotImplementedError("attention_mask is not used by the SD1.5 sampling path")
         x = _as_tokens(hidden_states)
         b, l, c = x.shape
         heads, d = attn.heads, attn.dim_head
         inner = heads * d
         ehs = encoder_hidden_states
         if ehs is None:  # self-attention use of the processor (reference :117-118)
-            return AttnProcessor.__call__(self, attn, hidden_states, None, None, temb, scale, _residual)
+            return AttnProcessor.__call__(self, attn, hidden_states, None, attention_mask, temb, scale, _residual)
         cache = cross_attention_kwargs.get("context_kv")
         kv = cache.get(attn) if cache is not None else None
         if kv is None:
@@ -177,7 +205,8 @@ class AudioAttnProcessor(nn.Module):
         q = ops.conv(x.view(b * l, c), attn.to_q.weight, attn.kpad_q, inner, ksize=1)
         if scale != 1.0:
             q.mul_(scale)
-        o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d)
+        o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d,
+                          key_bias=key_bias_of(attention_mask, b, heads, lk))
         out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
                              out=None if _residual is None else _residual.reshape(b * l, c))
         return out.view(b, l, c)

@@ -7,8 +7,11 @@ pipeline the reference drives loads (scripts/inference.py:30-33).
 
 No tokenizer vocabulary or weights exist offline, so prompts map to fixed,
 deterministic token-id lists (BOS, per-word ids from a stable hash, EOS, EOS
-padding to 77 as in SD1.5) and the tower is randomly initialised from a seed
-(the SD1.5 architecture: 12 layers, width 768, 12 heads, quick_gelu).
+padding to 77 as in SD1.5) and the tower loads a CLIPTextModel-keyed state dict,
+by default the seeded recipe weights.synth_clip_text (the SD1.5 architecture:
+12 layers, width 768, 12 heads, quick_gelu).  The product never imports
+transformers; the tests load the same state dict into transformers'
+CLIPTextModel as the fp32 oracle (oracle/clip_ref.py).
 """
 from __future__ import annotations
 
@@ -34,45 +37,38 @@ def tokenize(prompts: list[str], device=None) -> torch.Tensor:
     return torch.tensor([prompt_to_ids(p) for p in prompts], dtype=torch.long, device=device)
 
 
-def clip_text_model(seed: int = 0):
-    """The seeded random-init transformers CLIPTextModel (fp32, CPU): the weight source
-    of TextEncoder and, in tests, its fp32 oracle."""
-    from transformers import CLIPTextConfig, CLIPTextModel
-    cfg = CLIPTextConfig(vocab_size=VOCAB, hidden_size=768, intermediate_size=3072, num_hidden_layers=12,
-                         num_attention_heads=12, max_position_embeddings=MAXLEN, hidden_act="quick_gelu",
-                         projection_dim=768)
-    with torch.random.fork_rng(devices=[]):
-        torch.manual_seed(seed)
-        return CLIPTextModel(cfg).eval()
-
-
 class TextEncoder:
     HEADS, D = 12, 64
 
-    def __init__(self, device, seed: int = 0, model=None):
-        m = model or clip_text_model(seed)
-        m = getattr(m, "text_model", m)  # transformers < 5 wraps the tower
+    def __init__(self, device, seed: int = 0, state_dict: dict | None = None):
+        """Weights from a CLIPTextModel state dict (SD1.5 text_encoder keys, with or without
+        the "text_model." prefix); default: the seeded recipe weights.synth_clip_text(seed)."""
+        from .weights import synth_clip_text
+        sd = state_dict if state_dict is not None else synth_clip_text(seed)
+        sd = {(k[len("text_model."):] if k.startswith("text_model.") else k): v for k, v in sd.items()}
         dev = torch.device(device)
         self.device = dev
-        f32 = lambda t: t.detach().float().contiguous().to(dev)  # noqa: E731
-        self.tok = m.embeddings.token_embedding.weight.detach().half().to(dev)
-        self.pos = m.embeddings.position_embedding.weight.detach().half().to(dev)
+        f32 = lambda k: sd[k].detach().float().contiguous().to(dev)  # noqa: E731
+        self.tok = sd["embeddings.token_embedding.weight"].detach().half().to(dev)
+        self.pos = sd["embeddings.position_embedding.weight"].detach().half().to(dev)
         self.layers = []
-        for lyr in m.encoder.layers:
-            a = lyr.self_attn
+        n_layers = 1 + max(int(k.split(".")[2]) for k in sd if k.startswith("encoder.layers."))
+        for i in range(n_layers):
+            b = f"encoder.layers.{i}."
+            a = b + "self_attn."
             qkv = HLinear(768, 2304)
-            qkv.load(torch.cat([a.q_proj.weight, a.k_proj.weight, a.v_proj.weight]).detach(),
-                     torch.cat([a.q_proj.bias, a.k_proj.bias, a.v_proj.bias]).detach())
+            qkv.load(torch.cat([sd[a + "q_proj.weight"], sd[a + "k_proj.weight"], sd[a + "v_proj.weight"]]).float(),
+                     torch.cat([sd[a + "q_proj.bias"], sd[a + "k_proj.bias"], sd[a + "v_proj.bias"]]).float())
             out, fc1, fc2 = HLinear(768, 768), HLinear(768, 3072), HLinear(3072, 768)
-            out.load(a.out_proj.weight.detach(), a.out_proj.bias.detach())
-            fc1.load(lyr.mlp.fc1.weight.detach(), lyr.mlp.fc1.bias.detach())
-            fc2.load(lyr.mlp.fc2.weight.detach(), lyr.mlp.fc2.bias.detach())
+            out.load(sd[a + "out_proj.weight"].float(), sd[a + "out_proj.bias"].float())
+            fc1.load(sd[b + "mlp.fc1.weight"].float(), sd[b + "mlp.fc1.bias"].float())
+            fc2.load(sd[b + "mlp.fc2.weight"].float(), sd[b + "mlp.fc2.bias"].float())
             self.layers.append(dict(
-                ln1=(f32(lyr.layer_norm1.weight), f32(lyr.layer_norm1.bias)),
-                ln2=(f32(lyr.layer_norm2.weight), f32(lyr.layer_norm2.bias)),
+                ln1=(f32(b + "layer_norm1.weight"), f32(b + "layer_norm1.bias")),
+                ln2=(f32(b + "layer_norm2.weight"), f32(b + "layer_norm2.bias")),
                 qkv=qkv.to(dev), out=out.to(dev), fc1=fc1.to(dev), fc2=fc2.to(dev)))
-        self.lnf = (f32(m.final_layer_norm.weight), f32(m.final_layer_norm.bias))
-        self.eps = m.final_layer_norm.eps
+        self.lnf = (f32("final_layer_norm.weight"), f32("final_layer_norm.bias"))
+        self.eps = 1e-5   # CLIPTextConfig.layer_norm_eps
 
     @torch.no_grad()
     def __call__(self, ids: torch.Tensor) -> torch.Tensor:

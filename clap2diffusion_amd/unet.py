@@ -127,17 +127,21 @@ class BasicTransformerBlock(nn.Module):
         self.norm3 = HLayerNorm(dim)
         self.ff = FeedForward(dim)
 
-    def _attend(self, attn: Attention, x, h, ehs, kwargs):
+    def _attend(self, attn: Attention, x, h, ehs, mask, kwargs):
         if getattr(attn.processor, "fuses_residual", False):
-            return attn(x, encoder_hidden_states=ehs, _residual=h, **kwargs)
-        out = attn(x, encoder_hidden_states=ehs, **kwargs)
-        return ops.add(out.contiguous(), h)
+            return attn(x, encoder_hidden_states=ehs, attention_mask=mask, _residual=h, **kwargs)
+        # a diffusers-style processor (torch ops, e.g. the reference's own): its output
+        # plus the block residual, as BasicTransformerBlock adds it
+        out = attn(x, encoder_hidden_states=ehs, attention_mask=mask, **kwargs)
+        return ops.add(out.to(h.dtype).contiguous(), h)
 
-    def forward(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict) -> torch.Tensor:
-        """h: [B, L, C] fp16 (updated in place by the fused residual epilogues)."""
+    def forward(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict,
+                encoder_attention_mask: torch.Tensor | None = None) -> torch.Tensor:
+        """h: [B, L, C] fp16 (updated in place by the fused residual epilogues).
+        encoder_attention_mask: additive key bias for attn2 (diffusers BasicTransformerBlock)."""
         kw = cross_attention_kwargs or {}
-        h = self._attend(self.attn1, self.norm1(h), h, None, kw)
-        h = self._attend(self.attn2, self.norm2(h), h, ehs, kw)
+        h = self._attend(self.attn1, self.norm1(h), h, None, None, kw)
+        h = self._attend(self.attn2, self.norm2(h), h, ehs, encoder_attention_mask, kw)
         b, l, c = h.shape
         h2 = h.view(b * l, c)
         ff1 = self.ff.net[0].proj(self.norm3(h2), act="geglu")
@@ -153,10 +157,10 @@ class Transformer2DModel(nn.Module):
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(c, heads, cross_dim)])
         self.proj_out = HConv2d(c, c, 1)
 
-    def forward(self, x, ehs, cross_attention_kwargs):
+    def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None):
         n, hh, ww, c = x.shape
         h = self.proj_in(self.norm.apply(x))
-        t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs)
+        t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
         return self.proj_out(t.view(n, hh, ww, c), resid=x)
 
 
@@ -327,10 +331,13 @@ class UNet2DConditionModel(nn.Module):
 
     # ------------------------------------------------------------ forward
     def forward_nhwc(self, x: torch.Tensor, t_sin: torch.Tensor, ehs: torch.Tensor,
-                     cross_attention_kwargs: dict | None = None) -> torch.Tensor:
+                     cross_attention_kwargs: dict | None = None,
+                     encoder_attention_mask: torch.Tensor | None = None) -> torch.Tensor:
         """x: [N, H, W, 8] fp16 (latent zero-padded to 8 ch); t_sin: [N, 320] fp16
-        sinusoidal embedding; ehs: [N, 77, 768] fp16. Returns eps [N, H, W, 4] fp16."""
+        sinusoidal embedding; ehs: [N, 77, 768] fp16; encoder_attention_mask: additive
+        key bias [N, 1, 77] for every attn2 (or None). Returns eps [N, H, W, 4] fp16."""
         kw = cross_attention_kwargs or {}
+        em = encoder_attention_mask
         temb = self.time_embedding(t_sin)
         temb_all = ops.conv(temb, self.w_temb_all, self.temb_kpad, self.temb_total, ksize=1, bias=self.b_temb_all,
                             silu_in=True)
@@ -340,27 +347,30 @@ class UNet2DConditionModel(nn.Module):
             for j, r in enumerate(blk.resnets):
                 h = r(h, temb_all)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw)
+                    h = blk.attentions[j](h, ehs, kw, em)
                 skips.append(h)
             if hasattr(blk, "downsamplers"):
                 h = blk.downsamplers[0](h)
                 skips.append(h)
         mb = self.mid_block
         h = mb.resnets[0](h, temb_all)
-        h = mb.attentions[0](h, ehs, kw)
+        h = mb.attentions[0](h, ehs, kw, em)
         h = mb.resnets[1](h, temb_all)
         for blk in self.up_blocks:
             for j, r in enumerate(blk.resnets):
                 h = r(h, temb_all, skip=skips.pop())
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw)
+                    h = blk.attentions[j](h, ehs, kw, em)
             if hasattr(blk, "upsamplers"):
                 h = blk.upsamplers[0](h)
         return self.conv_out(self.conv_norm_out.apply(h, silu=True))
 
     def forward(self, sample: torch.Tensor, timestep, encoder_hidden_states: torch.Tensor,
-                cross_attention_kwargs: dict | None = None, return_dict: bool = True):
-        """diffusers-compatible entry: sample [N, 4, H, W] -> eps [N, 4, H, W] fp16."""
+                cross_attention_kwargs: dict | None = None, return_dict: bool = True,
+                encoder_attention_mask: torch.Tensor | None = None):
+        """diffusers-compatible entry: sample [N, 4, H, W] -> eps [N, 4, H, W] fp16.
+        encoder_attention_mask [N, 77] (1 = keep, 0 = discard) becomes the additive bias
+        (1 - mask) * -10000 of every cross-attention, as diffusers 0.23.1 builds it."""
         n = sample.shape[0]
         x = ops.latent_to_nhwc(sample.float().contiguous(), self.in_pad, dup=False)
         t = torch.as_tensor(timestep, dtype=torch.float32, device=sample.device).reshape(-1)
@@ -370,6 +380,9 @@ class UNet2DConditionModel(nn.Module):
             t_sin = torch.cat([ops.timestep_embedding(t[i:i + 1].contiguous(), None, 1,
                                                       self.cfg["block_out_channels"][0]) for i in range(n)])
         ehs = encoder_hidden_states.to(torch.float16).contiguous()
-        eps = self.forward_nhwc(x, t_sin, ehs, cross_attention_kwargs)
+        em = None
+        if encoder_attention_mask is not None:
+            em = ((1.0 - encoder_attention_mask.float()) * -10000.0).unsqueeze(1)
+        eps = self.forward_nhwc(x, t_sin, ehs, cross_attention_kwargs, em)
         out = eps.permute(0, 3, 1, 2).contiguous()
         return UNetOutput(out) if return_dict else (out,)

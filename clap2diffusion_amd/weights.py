@@ -300,6 +300,74 @@ def synth_htsat(seed: int = 0, device="cpu") -> "OrderedDict[str, torch.Tensor]"
     return synth_generic(htsat_param_shapes(), seed, "htsat.", device)
 
 
+def clap_audio_state_dict(ck: dict) -> "OrderedDict[str, torch.Tensor]":
+    """Audio-tower keys of a CLAP checkpoint, as HTSATEncoder.load_clap_state_dict takes
+    them (audio_model.audio_encoder.*, audio_projection.*).  Accepts a ClapModel state dict,
+    the reference's CLAPAudioEncoder state dict (models/audio_encoder.py:47: keys under
+    "clap_model."), or either wrapped in {"state_dict" | "model_state_dict": ...} -- the
+    forms a clap_encoder.pth (scripts/inference.py:38-41) can take."""
+    for wrap in ("state_dict", "model_state_dict"):
+        if isinstance(ck.get(wrap), dict):
+            ck = ck[wrap]
+    out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    for k, v in ck.items():
+        k2 = k[len("clap_model."):] if k.startswith("clap_model.") else k
+        if k2.startswith("audio_model.") or k2.startswith("audio_projection."):
+            out[k2] = v
+    if not out:
+        raise KeyError("no CLAP audio-tower keys (audio_model.* / audio_projection.*) in checkpoint")
+    return out
+
+
+# ------------------------------------------------------------------ CLIP text tower
+CLIP_TEXT_CFG = dict(vocab=49408, width=768, layers=12, heads=12, mlp=3072, max_len=77)
+
+
+def clip_text_param_shapes(cfg: dict = CLIP_TEXT_CFG) -> "OrderedDict[str, tuple]":
+    """CLIPTextModel keys of the SD1.5 text_encoder checkpoint (transformers 4.35
+    layout, "text_model." prefix; modeling_clip.py CLIPTextTransformer)."""
+    S: "OrderedDict[str, tuple]" = OrderedDict()
+    t, w, f = "text_model.", cfg["width"], cfg["mlp"]
+    S[t + "embeddings.token_embedding.weight"] = (cfg["vocab"], w)
+    S[t + "embeddings.position_embedding.weight"] = (cfg["max_len"], w)
+    for i in range(cfg["layers"]):
+        b = f"{t}encoder.layers.{i}."
+        for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            S[f"{b}self_attn.{n}.weight"] = (w, w)
+            S[f"{b}self_attn.{n}.bias"] = (w,)
+        S[b + "layer_norm1.weight"] = (w,)
+        S[b + "layer_norm1.bias"] = (w,)
+        S[b + "mlp.fc1.weight"] = (f, w)
+        S[b + "mlp.fc1.bias"] = (f,)
+        S[b + "mlp.fc2.weight"] = (w, f)
+        S[b + "mlp.fc2.bias"] = (w,)
+        S[b + "layer_norm2.weight"] = (w,)
+        S[b + "layer_norm2.bias"] = (w,)
+    S[t + "final_layer_norm.weight"] = (w,)
+    S[t + "final_layer_norm.bias"] = (w,)
+    return S
+
+
+def synth_clip_text(seed: int = 0, device="cpu") -> "OrderedDict[str, torch.Tensor]":
+    """Seeded CLIP text tower (Appendix B recipe): embeddings N(0, 0.02^2) (CLIP's own
+    init scale), linears N(0, 1/fan_in), LayerNorm gamma 1 + 0.1 N, beta 0.1 N."""
+    sd: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    g = torch.Generator(device=device)
+    for k, shp in clip_text_param_shapes().items():
+        g.manual_seed(key_seed(seed, "clip." + k))
+        r = torch.randn(shp, generator=g, device=device)
+        if "embedding" in k:
+            v = 0.02 * r
+        elif "layer_norm" in k:
+            v = (1.0 + 0.1 * r) if k.endswith(".weight") else 0.1 * r
+        elif k.endswith(".bias"):
+            v = 0.02 * r
+        else:
+            v = r / math.sqrt(shp[1])
+        sd[k] = v
+    return sd
+
+
 def fill_module(module, tag: str, seed: int = 0, keep=("decomposer.temperature", "decomposer.level_prior")):
     """Deterministically (re)initialise every floating tensor of a torch module by key."""
     sd = module.state_dict()

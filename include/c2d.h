@@ -106,6 +106,16 @@ int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
 size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d);
 
 /*
+ * The kernel plan c2d_conv2d_igemm would run for this descriptor (no launch, no device
+ * access): tile_id = the LDS-DMA tile configuration (0 = the register-staged kernel of
+ * descriptors with a prologue / upsampled view), ksplit = K slices (1 = no split-K;
+ * reflects d->ws / d->ws_bytes as the launch would).  Lets callers and the per-tile
+ * parity test (tests/test_kernels_gpu.py) see which kernel ran; C2D_GEMM_TILE /
+ * C2D_GEMM_SPLIT in the environment override the planner (tuning and tests only).
+ */
+int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit);
+
+/*
  * GroupNorm statistics folded with the affine into per-(image, channel) scale /
  * shift tables consumed by the C2D_PRO_GN prologue:
  *   scale[n][c] = gamma[c]*rstd[n,g(c)], shift[n][c] = beta[c] - mean[n,g(c)]*scale[n][c]
@@ -176,6 +186,20 @@ int c2d_attention_fwd(const void* q, int ldq, const void* k, int ldk, const void
                       float scale, int kv_div, void* stream);
 
 /*
+ * c2d_attention_fwd with an additive per-key score bias (the attention_mask of the
+ * processor API, reference models/audio_attention_processor.py:48,129 -> diffusers
+ * Attention.get_attention_scores, baddbmm(mask, q, k^T, beta=1, alpha=scale), in the
+ * key-padding form diffusers builds from encoder_attention_mask, (1 - keep) * -10000):
+ *   S[b, h, i, j] = Q.K * scale + key_bias[b * bias_ld_batch + h * bias_ld_head + j]
+ * fp32 bias, natural-log units; strides 0 broadcast over images / heads.  key_bias NULL
+ * is exactly c2d_attention_fwd.  Per-query masks are not representable here.
+ */
+int c2d_attention_fwd_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                           void* o, int ldo, int batch, int heads, int lq, int lk, int d, float scale,
+                           int kv_div, const float* key_bias, int bias_ld_batch, int bias_ld_head,
+                           void* stream);
+
+/*
  * Swin window attention of the HTSAT tower: tokens gathered through row_map
  * (window w, token t -> row of the [B*H*W] token matrix; encodes the cyclic
  * shift + window partition), 64-token windows, head dim 24, relative-position
@@ -217,14 +241,16 @@ int c2d_l2_normalize(float* x, int m, int c, void* stream);
 int c2d_attention_small(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o,
                         int ldo, int batch, int heads, int l, int d, float scale, int causal, void* stream);
 
-/* CLAP log-mel front end (transformers ClapFeatureExtractor, truncation "rand_trunc",
- * padding "repeatpad": feature_extraction_clap.py _get_input_mel + audio_utils.spectrogram
- * with a periodic Hann window, centre reflect pad, power 2, mel filters, dB; called from
- * the reference's models/audio_encoder.py:163-167).  wave: fp32 clips concatenated,
- * clip i at wave + offsets[i] with lengths[i] (1 <= len <= max_len; a longer clip is
- * cropped by the caller with the extractor's np.random.randint offset).  window fp32
- * [n_fft]; mel_filters fp32 [n_mels][n_fft/2+1]; filter_range int [n_mels][2] = the
- * non-zero bin range [lo, hi) of each filter.  out fp32 [b][1 + max_len/hop][n_mels].
+/* CLAP log-mel front end: the reference's audio composition -- CLAPAudioEncoder.preprocess_audio
+ * (models/audio_encoder.py:121-129: zero-pad to max_len = 10 s x 48 kHz samples, or keep the
+ * first max_len) then transformers ClapFeatureExtractor on that exact-length clip
+ * (feature_extraction_clap.py _get_input_mel: no repeat-pad / crop at exact length;
+ * audio_utils.spectrogram with a periodic Hann window, centre reflect pad, power 2, mel
+ * filters, dB; models/audio_encoder.py:163-167).  wave: fp32 clips concatenated, clip i at
+ * wave + offsets[i] with lengths[i] samples; lengths are clamped to [0, max_len] on the
+ * device (longer -> first max_len samples, 0 -> silence = -100 dB), so no length can fault.
+ * window fp32 [n_fft]; mel_filters fp32 [n_mels][n_fft/2+1]; filter_range int [n_mels][2] =
+ * the non-zero bin range [lo, hi) of each filter.  out fp32 [b][1 + max_len/hop][n_mels].
  * n_fft must be 1024. */
 int c2d_clap_log_mel(const float* wave, const long long* offsets, const int* lengths, int b, int max_len,
                      int n_fft, int hop, const float* window, const float* mel_filters,

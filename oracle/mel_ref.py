@@ -1,13 +1,16 @@
 """CLAP log-mel oracle -- TEST INFRASTRUCTURE ONLY (float64 numpy).
 
-Restates the work of transformers' ClapFeatureExtractor(truncation="rand_trunc",
-padding="repeatpad") on ONE already-cropped clip (the random crop of longer clips
-is host work shared with the product): feature_extraction_clap.py
-_get_input_mel (repeatpad: np.tile max_len // n times, zero tail) and
-_np_extract_fbank_features -> audio_utils.spectrogram(window_function(1024,
-"hann") periodic, frame 1024, hop 480, power 2, centre reflect pad, mel filters
-(Slaney scale + norm), log_mel "dB" = power_to_db: 10 log10(max(x, 1e-10))).
-The reference calls it through ClapProcessor at models/audio_encoder.py:163-167.
+Restates the reference's audio composition on ONE clip:
+  preprocess(): CLAPAudioEncoder.preprocess_audio (models/audio_encoder.py:109-129):
+    mono mean, zero-pad to max_len samples (np.pad mode "constant") or keep the first
+    max_len;
+  log_mel(): transformers ClapFeatureExtractor on that exact-length clip
+    (feature_extraction_clap.py _get_input_mel -- at exact length neither repeat-pad
+    nor the random crop fires -- and _np_extract_fbank_features ->
+    audio_utils.spectrogram(window_function(1024, "hann") periodic, frame 1024, hop
+    480, power 2, centre reflect pad, mel filters (Slaney scale + norm), log_mel "dB"
+    = power_to_db: 10 log10(max(x, 1e-10)))), called by the reference through
+    ClapProcessor at models/audio_encoder.py:163-167.
 Pinned against transformers itself by tests/test_mel_cpu.py and the fixture
 tests/golden/mel.npz (scripts/make_mel_golden.py).
 """
@@ -35,14 +38,20 @@ def slaney_filters(n_bins: int, n_mels: int, fmin: float, fmax: float, sr: int) 
     return fb
 
 
+def preprocess(clip: np.ndarray, max_len: int = 480_000) -> np.ndarray:
+    """models/audio_encoder.py:109-129: mono, then zero-pad / truncate to max_len."""
+    x = np.asarray(clip, np.float64)
+    if x.ndim > 1:
+        x = x.mean(axis=-1)
+    if x.size < max_len:
+        return np.pad(x, (0, max_len - x.size), mode="constant")
+    return x[:max_len]
+
+
 def log_mel(clip: np.ndarray, max_len: int = 480_000, sr: int = 48_000, n_fft: int = 1024, hop: int = 480,
             n_mels: int = 64, fmin: float = 0.0, fmax: float = 14_000.0) -> np.ndarray:
-    """clip (len <= max_len) -> [1 + max_len // hop, n_mels] float64 dB features."""
-    x = np.asarray(clip, np.float64)
-    assert 0 < x.size <= max_len
-    w = np.zeros(max_len)
-    reps = max_len // x.size
-    w[: reps * x.size] = np.tile(x, reps)
+    """clip (any length) -> preprocess -> [1 + max_len // hop, n_mels] float64 dB features."""
+    w = preprocess(clip, max_len)
     w = np.pad(w, n_fft // 2, mode="reflect")
     win = np.hanning(n_fft + 1)[:-1]
     frames = 1 + (w.size - n_fft) // hop

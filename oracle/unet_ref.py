@@ -81,7 +81,9 @@ class UNetRef:
             x = self.conv(pre + ".conv_shortcut", x)
         return x + h
 
-    def attention(self, pre, x, ctx):
+    def attention(self, pre, x, ctx, bias=None):
+        """bias: additive score bias broadcast to [b, heads, lq, lk] (diffusers
+        get_attention_scores adds attention_mask to q k^T * scale)."""
         c = x.shape[-1]
         h = self.heads
         d = c // h
@@ -96,6 +98,8 @@ class UNetRef:
         o = torch.empty_like(q)
         for i in range(0, lq, 2048):   # query blocks: bounded score memory at 96^2 (c5)
             s = torch.matmul(q[:, :, i:i + 2048], k.transpose(-1, -2)) * (d ** -0.5)
+            if bias is not None:
+                s = s + bias
             o[:, :, i:i + 2048] = torch.matmul(s.softmax(-1), v)
         o = o.transpose(1, 2).reshape(b, lq, c)
         return self.lin(pre + ".to_out.0", o)
@@ -113,7 +117,7 @@ class UNetRef:
         gate = torch.sigmoid(w["alpha"].float())
         return ehs + gate * pooled
 
-    def transformer(self, pre, x, ehs, audio):
+    def transformer(self, pre, x, ehs, audio, mask_bias=None):
         b, c, hh, ww = x.shape
         res = x
         h = self.conv(pre + ".proj_in", self.gn(pre + ".norm", x, 1e-6))
@@ -123,16 +127,21 @@ class UNetRef:
         h = self.attention(blk + ".attn1", n, n) + h
         n = self.ln(blk + ".norm2", h)
         ctx = self.audio_context(level_of(pre), ehs, audio)
-        h = self.attention(blk + ".attn2", n, ctx) + h
+        h = self.attention(blk + ".attn2", n, ctx, mask_bias) + h
         n = self.ln(blk + ".norm3", h)
         hid, gate = self.lin(blk + ".ff.net.0.proj", n).chunk(2, dim=-1)
         h = self.lin(blk + ".ff.net.2", hid * F.gelu(gate)) + h
         h = h.reshape(b, hh, ww, c).permute(0, 3, 1, 2)
         return self.conv(pre + ".proj_out", h) + res
 
-    def __call__(self, sample, t, ehs, audio=None):
-        """sample [N,4,H,W] fp32, t scalar or [N], ehs [N,77,768], audio {level: [N,K,768]}."""
+    def __call__(self, sample, t, ehs, audio=None, encoder_attention_mask=None):
+        """sample [N,4,H,W] fp32, t scalar or [N], ehs [N,77,768], audio {level: [N,K,768]};
+        encoder_attention_mask [N, 77] keep-mask -> (1 - m) * -10000 bias on every attn2
+        (diffusers 0.23.1 UNet2DConditionModel.forward)."""
         n = sample.shape[0]
+        mb = None
+        if encoder_attention_mask is not None:
+            mb = ((1.0 - encoder_attention_mask.float()) * -10000.0)[:, None, None, :]
         t = torch.as_tensor(t, dtype=torch.float32).reshape(-1).expand(n)
         temb = timestep_embedding(t, self.p("conv_in.weight").shape[0])
         temb = self.lin("time_embedding.linear_2", F.silu(self.lin("time_embedding.linear_1", temb)))
@@ -143,20 +152,20 @@ class UNetRef:
             for j in range(2):
                 h = self.resnet(f"down_blocks.{i}.resnets.{j}", h, temb)
                 if f"down_blocks.{i}.attentions.{j}.norm.weight" in self.sd:
-                    h = self.transformer(f"down_blocks.{i}.attentions.{j}", h, ehs, audio)
+                    h = self.transformer(f"down_blocks.{i}.attentions.{j}", h, ehs, audio, mb)
                 skips.append(h)
             if f"down_blocks.{i}.downsamplers.0.conv.weight" in self.sd:
                 h = self.conv(f"down_blocks.{i}.downsamplers.0.conv", h, stride=2)
                 skips.append(h)
         h = self.resnet("mid_block.resnets.0", h, temb)
-        h = self.transformer("mid_block.attentions.0", h, ehs, audio)
+        h = self.transformer("mid_block.attentions.0", h, ehs, audio, mb)
         h = self.resnet("mid_block.resnets.1", h, temb)
         for i in range(nblocks):
             for j in range(3):
                 h = torch.cat([h, skips.pop()], dim=1)
                 h = self.resnet(f"up_blocks.{i}.resnets.{j}", h, temb)
                 if f"up_blocks.{i}.attentions.{j}.norm.weight" in self.sd:
-                    h = self.transformer(f"up_blocks.{i}.attentions.{j}", h, ehs, audio)
+                    h = self.transformer(f"up_blocks.{i}.attentions.{j}", h, ehs, audio, mb)
             if f"up_blocks.{i}.upsamplers.0.conv.weight" in self.sd:
                 h = F.interpolate(h, scale_factor=2.0, mode="nearest")
                 h = self.conv(f"up_blocks.{i}.upsamplers.0.conv", h)

@@ -1,14 +1,18 @@
 #!/bin/bash
-# One GPU call: gpu tests, then the default bench.  Stops at a fault / abort / timeout.
+# One GPU call: gpu tests (PYTEST_K selects a subset), then the bench unless NOBENCH=1.
+# Stops at a fault / abort / timeout.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+K=()
+[ -n "$PYTEST_K" ] && K=(-k "$PYTEST_K")
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${K[@]}" > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
-echo "pytest exit $rc"; tail -5 gpurun_out/pytest_gpu.log
+echo "pytest exit $rc"; grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_gpu.log | tail -3; tail -5 gpurun_out/pytest_gpu.log
 case $rc in 0|1) ;; *) exit $rc ;; esac
-timeout -k 10 400 python -u bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err
+[ -n "$NOBENCH" ] && exit $rc
+timeout -k 10 ${BENCH_TIMEOUT:-500} python -u bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?
 tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json
 exit $rc

@@ -126,6 +126,48 @@ def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
     close(nchw(out), ref)
 
 
+# every tile configuration left in igemm.hip's kDmaTiles, forced through C2D_GEMM_TILE
+# (read per launch) and confirmed through c2d_conv2d_igemm_plan
+DMA_TILE_IDS = [25, 28, 29, 7, 1, 2, 3]
+
+
+@pytest.mark.parametrize("tile", DMA_TILE_IDS)
+@pytest.mark.parametrize("k,split", [(3, 1), (1, 1), (3, 2)])
+def test_every_dma_tile_forced(dev, monkeypatch, tile, k, split):
+    n, h, cin, cout = 4, 16, 320, 640
+    monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
+    monkeypatch.setenv("C2D_GEMM_SPLIT", str(split))
+    x = gen(n, cin, h, h, seed=91)
+    w = gen(cout, cin, k, k, seed=92, scale=1.0 / math.sqrt(k * k * cin))
+    b = gen(cout, seed=93)
+    resid = gen(n, cout, h, h, seed=94)
+    ref = F.conv2d(x, w, b, padding=k // 2) + resid
+    wp, kp = ops.pack_conv_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(nhwc(x).half().to(dev), wp.to(dev), kp, cout, ksize=k, bias=b.float().to(dev),
+                       resid=nhwc(resid).half().to(dev))
+    assert plans == [(tile, split)], plans
+    close(nchw(out), ref)
+
+
+@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t != 7])   # 7 (odd column tiles) skips GEGLU
+def test_every_dma_tile_forced_geglu(dev, monkeypatch, tile):
+    m, cin, inner = 1024, 320, 640
+    monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
+    monkeypatch.setenv("C2D_GEMM_SPLIT", "1")
+    x = gen(m, cin, seed=95)
+    w = gen(2 * inner, cin, seed=96, scale=1.0 / math.sqrt(cin))
+    b = gen(2 * inner, seed=97)
+    hh, gg = (x @ w.t() + b).chunk(2, -1)
+    ref = hh * F.gelu(gg)
+    wi, bi = ops.geglu_interleave(w, b)
+    wp, kp = ops.pack_linear_weight(wi)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(x.half().to(dev), wp.to(dev), kp, 2 * inner, ksize=1, bias=bi.float().to(dev), act="geglu")
+    assert plans == [(tile, 1)], plans
+    close(out, ref)
+
+
 @pytest.mark.parametrize("n,h,c0,c1,cout,k", [
     (2, 8, 1280, 640, 640, 3),      # 64x64 DMA tiles
     (16, 32, 640, 320, 320, 3),     # 128x128 DMA tiles
@@ -337,6 +379,32 @@ def test_attention_spike(dev):
     close(out, ref)
 
 
+@pytest.mark.parametrize("b,h,lq,lk,d,form", [
+    (2, 8, 300, 77, 40, "per_image"),     # cross-attention with a key-padding mask (resident K/V)
+    (2, 8, 256, 77, 160, "per_head"),
+    (1, 8, 1024, 1024, 80, "broadcast"),  # self-attention, streaming K/V
+    (2, 4, 200, 333, 40, "per_image"),
+])
+def test_attention_key_bias(dev, b, h, lq, lk, d, form):
+    q, k, v = gen(b * lq, h * d, seed=61), gen(b * lk, h * d, seed=62), gen(b * lk, h * d, seed=63)
+    g = torch.Generator().manual_seed(64)
+    if form == "per_image":
+        bias = torch.zeros(b, 1, lk)
+        for i in range(b):
+            bias[i, 0, (17 + 29 * i) % lk:] = -10000.0
+    elif form == "per_head":
+        bias = torch.randn(b, h, lk, generator=g) * 2.0
+    else:
+        bias = torch.randn(1, 1, lk, generator=g)
+    qh = q.view(b, lq, h, d).transpose(1, 2)
+    kh = k.view(b, lk, h, d).transpose(1, 2)
+    vh = v.view(b, lk, h, d).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=bias[:, :, None, :]).transpose(1, 2).reshape(b * lq, h * d)
+    out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d,
+                        key_bias=bias.to(dev))
+    close(out, ref)
+
+
 @pytest.mark.parametrize("d", [40, 80, 160])
 def test_attention_wide_scores(dev, d):
     # scores of std ~12 (log2 units ~17): the first key tile rebases the running max
@@ -533,13 +601,13 @@ def test_attention_small(dev, b, l, causal):
 
 
 def test_clip_text_tower(dev):
-    # HIP CLIP ViT-L/14 text tower vs the seeded transformers CLIPTextModel in fp32
-    from clap2diffusion_amd.text_encoder import TextEncoder, clip_text_model, tokenize
+    # HIP CLIP ViT-L/14 text tower vs transformers' CLIPTextModel in fp32, both loading
+    # the seeded CLIPTextModel-keyed state dict (weights.synth_clip_text)
+    from clap2diffusion_amd.text_encoder import TextEncoder, tokenize
+    from oracle.clip_ref import encode
     ids = tokenize(["", "a beach", "thunder over a dark city street at night"])
-    model = clip_text_model(0)
-    with torch.no_grad():
-        ref = model(input_ids=ids).last_hidden_state
-    out = TextEncoder(dev, model=model)(ids)
+    ref = encode(ids, seed=0)
+    out = TextEncoder(dev, seed=0)(ids)
     assert out.shape == ref.shape and out.dtype == torch.float16
     close(out, ref, tol_max=3e-2, tol_l2=1e-2)
 

@@ -22,24 +22,44 @@ TOL_DB = 2e-2
 def test_log_mel_matches_golden(dev):
     from clap2diffusion_amd.features import ClapLogMel
     from clap2diffusion_amd.pipeline import synthetic_thunder
+    # exact, short (zero tail) and long (first second kept) clips, as the reference composes them
     g = np.load(ROOT / "tests" / "golden" / "mel.npz")
     fe = ClapLogMel(dev, max_length_s=1)
     for (s, n), ref in zip(g["recipe"], g["features"]):
-        np.random.seed(1234)  # the fixture's crop offset for the longer clip
         out = fe([synthetic_thunder(int(s), int(n) / 48_000)])[0].cpu().numpy()
         assert np.abs(out - ref).max() < TOL_DB
 
 
 def test_log_mel_batch_full_length(dev):
-    # configs' 10 s / 48 kHz clips, mixed lengths in one launch (exact, repeatpad, short)
+    # configs' 10 s / 48 kHz clips, mixed lengths in one launch: exact, short clips zero-padded
+    # to 10 s (models/audio_encoder.py:123-126), a 12 s clip truncated to its first 10 s (:127-129)
     from clap2diffusion_amd.features import ClapLogMel
     from clap2diffusion_amd.pipeline import synthetic_thunder
-    clips = [synthetic_thunder(0, 10.0), synthetic_thunder(1, 3.3), synthetic_thunder(2, 0.05)]
+    clips = [synthetic_thunder(0, 10.0), synthetic_thunder(1, 3.3), synthetic_thunder(2, 0.05),
+             synthetic_thunder(3, 12.0)]
     fe = ClapLogMel(dev)
     out = fe(clips).cpu().numpy()
-    assert out.shape == (3, 1001, 64)
+    assert out.shape == (4, 1001, 64)
     for c, o in zip(clips, out):
         assert np.abs(o - log_mel(c)).max() < TOL_DB
+    # short clip == its explicit zero-padded 10 s version
+    pad = np.zeros(480_000, np.float32)
+    pad[: clips[1].size] = clips[1]
+    assert np.abs(out[1] - fe([pad]).cpu().numpy()[0]).max() == 0.0
+
+
+def test_log_mel_device_lengths_clamped(dev):
+    # from_device with lengths outside [1, max_len]: clamped on the device (no fault, no garbage)
+    from clap2diffusion_amd.features import ClapLogMel
+    from clap2diffusion_amd.pipeline import synthetic_thunder
+    fe = ClapLogMel(dev, max_length_s=1)
+    c = synthetic_thunder(4, 1.5)
+    wave = torch.from_numpy(np.concatenate([c, c])).to(dev)
+    offs = torch.tensor([0, c.size], dtype=torch.int64, device=dev)
+    lens = torch.tensor([c.size, 0], dtype=torch.int32, device=dev)
+    out = fe.from_device(wave, offs, lens).cpu().numpy()
+    assert np.abs(out[0] - log_mel(c, max_len=48_000)).max() < TOL_DB
+    assert np.all(np.abs(out[1] + 100.0) < 1e-4)
 
 
 def test_log_mel_silence_floor(dev):

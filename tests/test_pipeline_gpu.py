@@ -7,9 +7,9 @@ import math
 import pytest
 import torch
 
-from clap2diffusion_amd.pipeline import AudioToImageInference, synthetic_thunder
+from clap2diffusion_amd.pipeline import AudioToImageInference, initial_latents, synthetic_thunder
 from clap2diffusion_amd.text_encoder import tokenize
-from oracle.pipeline_ref import reference_images
+from oracle.pipeline_ref import ReferencePipeline, reference_images
 
 pytestmark = pytest.mark.gpu
 
@@ -30,7 +30,7 @@ def test_pipeline_matches_oracle_10_steps(pipe, dev):
     ids = (tokenize([""] * b, dev), tokenize(["a beach", "a forest"], dev))
     lat = pipe.initial_latents([0, 1])
     img = pipe.generate_batch(mel, None, 10, 7.5, ids=ids, latents=lat).cpu()
-    lat_hip = pipe._denoisers[(b, 10, 7.5)].x.cpu()
+    lat_hip = pipe.last_denoiser.x.cpu()
     ref, lat_ref = reference_images(mel.cpu(), ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10)
     rel = ((lat_hip - lat_ref).norm() / lat_ref.norm()).item()
     p = psnr(img, ref)
@@ -57,7 +57,7 @@ def test_graph_replay_is_repeatable(pipe, dev):
     ids = (tokenize([""] * b, dev), tokenize(["a beach"] * b, dev))
     lat = pipe.initial_latents([3, 4])
     outs = [pipe.generate_batch(mel, None, 10, 7.5, ids=ids, latents=lat) for _ in range(3)]
-    x = pipe._denoisers[(b, 10, 7.5)].x
+    x = pipe.last_denoiser.x
     assert torch.isfinite(x).all()
     for o in outs[1:]:
         assert (o.int() - outs[0].int()).abs().max().item() <= 2
@@ -72,3 +72,36 @@ def test_reference_api_surface(pipe, tmp_path):
     assert emb.shape == (1, 512) and abs(emb.norm().item() - 1.0) < 1e-3
     tok = pipe.apply_normalization(torch.randn(1, 16, 768, device=emb.device))
     assert abs(tok.norm(dim=-1).mean().item() - 60.0) < 1e-2
+
+
+@pytest.mark.timeout(900)
+def test_c1_workload_512_10_steps_from_waveform(pipe, dev):
+    # BASELINE.json c1's workload (1 x 512^2, 10 DDIM steps, "Thunder" + "a beach") end to end
+    # from the 48 kHz waveform: HIP log-mel -> ... -> VAE against the fp32 oracle pipeline
+    # (oracle log-mel from the same waveform): PSNR >= 30 dB, mean |diff| <= 3/255
+    wave = synthetic_thunder(0)
+    mel = pipe.mel_features([wave])
+    ids = (tokenize([""], dev), tokenize(["a beach"], dev))
+    lat = initial_latents([0], 64, 64, dev)
+    img = pipe.generate_batch(mel, None, 10, 7.5, ids=ids, latents=lat).cpu()
+    assert img.shape == (1, 512, 512, 3)
+    ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10)
+    p = psnr(img, ref)
+    mad = (img.float() - ref.float()).abs().mean().item()
+    assert p >= 30.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+
+
+def test_clap_encoder_checkpoint_is_loaded(dev, tmp_path):
+    # reference scripts/inference.py:38-41: clap_encoder.pth in checkpoint_dir drives the CLAP
+    # tower (here a CLAPAudioEncoder-style state dict, keys under "clap_model.")
+    from clap2diffusion_amd import weights as W
+    from oracle.htsat_ref import htsat_forward
+    sd = W.synth_htsat(5)
+    torch.save({"clap_model." + k: v for k, v in sd.items()}, tmp_path / "clap_encoder.pth")
+    p = AudioToImageInference(checkpoint_dir=tmp_path, device=dev, height=128, width=128, verbose=False)
+    mel = p.mel_features([synthetic_thunder(2)])
+    emb = p.clap(mel).float().cpu()
+    ref = htsat_forward(sd, mel.cpu()[:, None].float())
+    other = htsat_forward(W.synth_htsat(0), mel.cpu()[:, None].float())
+    cos = torch.nn.functional.cosine_similarity(emb, ref).item()
+    assert cos >= 0.999 and torch.nn.functional.cosine_similarity(emb, other).item() < 0.99

@@ -3,7 +3,9 @@ same synthetic SD1.5 weights, with the audio-injecting processors routed by
 AudioProcessorManager.  Tolerance: eps rel-L2 <= 1e-2."""
 import pytest
 import torch
+import torch.nn as nn
 
+from clap2diffusion_amd import ops
 from clap2diffusion_amd.processor import AudioProcessorManager
 from clap2diffusion_amd.unet import UNet2DConditionModel
 from clap2diffusion_amd.weights import synth_processor_weights, synth_unet
@@ -75,3 +77,103 @@ def test_attn_processor_names_and_levels(unet_pair):
     assert len(mgr.level_mapping["early"]) == 4
     assert len(mgr.level_mapping["mid"]) == 7
     assert len(mgr.level_mapping["late"]) == 5
+
+
+@pytest.mark.timeout(600)
+def test_unet_step_c3_batch_matches_oracle(dev, unet_pair):
+    # c3's UNet call as the bench runs it: N = 16 (CFG pair x 8 images) at 64x64 with audio,
+    # through the planner's full-chip routes (256x320 tiles, split-K at the 16^2 / 8^2 levels)
+    hip, ref, mgr = unet_pair
+    g = torch.Generator().manual_seed(316)
+    n = 16
+    x = torch.randn(n, 4, 64, 64, generator=g)
+    ehs = torch.randn(n, 77, 768, generator=g)
+    audio = {lv: torch.randn(n, 10, 768, generator=g) * 0.5 for lv in ("early", "mid", "late")}
+    with torch.no_grad(), ops.record_conv_plans() as plans:
+        e_hip = hip(x.to(dev), 981, ehs.to(dev),
+                    cross_attention_kwargs=mgr.get_audio_kwargs({k: v.to(dev) for k, v in audio.items()})).sample
+    torch.cuda.synchronize()
+    tiles = {t for t, _ in plans}
+    assert 25 in tiles and any(ks > 1 for _, ks in plans), (tiles, plans[:8])
+    with torch.no_grad():
+        e_ref = ref(x, 981, ehs, audio)
+    err = rel_l2(e_hip, e_ref)
+    assert err <= 1e-2, f"eps rel-L2 {err:.3e}"
+
+
+def test_unet_encoder_attention_mask_matches_oracle(dev, unet_pair):
+    # diffusers' encoder_attention_mask (keep-mask [N, 77]) -> additive key bias on every attn2
+    hip, ref, mgr = unet_pair
+    g = torch.Generator().manual_seed(41)
+    n = 2
+    x = torch.randn(n, 4, 16, 16, generator=g)
+    ehs = torch.randn(n, 77, 768, generator=g)
+    audio = {lv: torch.randn(n, 10, 768, generator=g) * 0.5 for lv in ("early", "mid", "late")}
+    keep = torch.ones(n, 77)
+    keep[0, 9:] = 0.0     # image 0: 9 real tokens, image 1: 30
+    keep[1, 30:] = 0.0
+    with torch.no_grad():
+        e_ref = ref(x, 601, ehs, audio, encoder_attention_mask=keep)
+        e_nomask = ref(x, 601, ehs, audio)
+        e_hip = hip(x.to(dev), 601, ehs.to(dev), encoder_attention_mask=keep.to(dev),
+                    cross_attention_kwargs=mgr.get_audio_kwargs({k: v.to(dev) for k, v in audio.items()})).sample
+    assert rel_l2(e_nomask, e_ref) > 5e-2       # the mask matters at this tolerance
+    assert rel_l2(e_hip, e_ref) <= 1e-2
+
+
+class TorchAudioProcessor(nn.Module):
+    """A diffusers-style processor written with torch ops on the Attention surface
+    (to_q / to_k / to_v / to_out, head_to_batch_dim, get_attention_scores,
+    batch_to_head_dim), following the reference AudioAttnProcessor's Add-FiLM
+    semantics (models/audio_attention_processor.py:76-145)."""
+
+    def __init__(self, level, w):
+        super().__init__()
+        self.level = level
+        self.audio_proj = nn.Sequential(nn.Linear(768, 64), nn.GELU(), nn.Dropout(0.1), nn.Linear(64, 768))
+        self.audio_proj[0].weight.data.copy_(w["audio_proj.0.weight"])
+        self.audio_proj[0].bias.data.copy_(w["audio_proj.0.bias"])
+        self.audio_proj[3].weight.data.copy_(w["audio_proj.3.weight"])
+        self.audio_proj[3].bias.data.copy_(w["audio_proj.3.bias"])
+        self.alpha = nn.Parameter(w["alpha"].clone())
+
+    def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
+                 scale=1.0, **kw):
+        audio = kw.get("audio")
+        ctx = encoder_hidden_states
+        if audio is not None and self.level in audio:
+            a = self.audio_proj(audio[self.level].float())
+            ctx = (ctx.float() + torch.sigmoid(self.alpha) * a.mean(dim=1, keepdim=True)).to(torch.float16)
+        q = attn.to_q(hidden_states) * scale
+        k, v = attn.to_k(ctx.contiguous()), attn.to_v(ctx.contiguous())
+        q, k, v = attn.head_to_batch_dim(q), attn.head_to_batch_dim(k), attn.head_to_batch_dim(v)
+        probs = attn.get_attention_scores(q.float(), k.float(), attention_mask)
+        h = attn.batch_to_head_dim(torch.bmm(probs, v.float())).to(torch.float16)
+        return attn.to_out[1](attn.to_out[0](h.contiguous()))
+
+
+def test_diffusers_style_torch_processor_in_hip_unet(dev, unet_pair):
+    # a torch processor plugged into the HIP UNet through set_attn_processor gives the same
+    # eps as the HIP processors (oracle-checked), then the HIP processors are restored
+    hip, ref, mgr = unet_pair
+    saved = dict(hip.attn_processors)
+    procs = dict(saved)
+    for level, names in mgr.level_mapping.items():
+        tp = TorchAudioProcessor(level, synth_processor_weights(level, seed=0)).to(dev).eval()
+        for name in names:
+            procs[name] = tp
+    g = torch.Generator().manual_seed(53)
+    n = 2
+    x = torch.randn(n, 4, 16, 16, generator=g)
+    ehs = torch.randn(n, 77, 768, generator=g)
+    audio = {lv: torch.randn(n, 10, 768, generator=g) * 0.5 for lv in ("early", "mid", "late")}
+    try:
+        hip.set_attn_processor(procs)
+        with torch.no_grad():
+            e_hip = hip(x.to(dev), 421, ehs.to(dev),
+                        cross_attention_kwargs={"audio": {k: v.to(dev) for k, v in audio.items()}}).sample
+    finally:
+        hip.set_attn_processor(saved)
+    with torch.no_grad():
+        e_ref = ref(x, 421, ehs, audio)
+    assert rel_l2(e_hip, e_ref) <= 1e-2
