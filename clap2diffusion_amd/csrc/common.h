@@ -16,6 +16,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_AS __attribute__((address_space(3)))
 
+
+
 // Timing-ablation switches (C2D_GEMM_ABL / C2D_ATTN_ABL: skip the DMA, the MFMAs or
 // the epilogue to attribute kernel time; wrong results by design) exist only in a
 // bench build compiled with -DC2D_ENABLE_ABLATION (scripts/gpu_gemm_abl.sh).  In the

@@ -661,6 +661,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
 
 }  // namespace c2d
 #include "igemm_m32.h"
+#include "igemm_pp16.h"
 namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -731,6 +732,8 @@ struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
 static const DmaTile kDmaTiles[] = {
     // 32x32x16 MFMA, LDS-DMA ring (igemm_m32.h); rate 0 = chosen by the rules in plan_for only
     {25, 256, 320, 1, 0.0f, true},
+    {40, 256, 320, 1, 0.0f, false},   // ping-pong 16x16x32 (80-column wave tiles: no GEGLU pairs)
+    {41, 256, 256, 1, 0.0f, true},
     {28, 256, 256, 1, 0.0f, true},
     {29, 256, 128, 1, 0.0f, true},
     // 16x16x32 MFMA LDS-DMA family, costed by plan_dma
@@ -835,14 +838,19 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     // 256 / 512 ch: 11-14 % faster)
     if (!geglu && cout % 320 != 0) {
         const long mt = (M + 255) / 256;
-        if (cout % 256 == 0 && mt * (cout / 256) >= 192) return {28, 1, nk};
+        if (cout % 256 == 0 && mt * (cout / 256) >= 192) return {41, 1, nk};   // ping-pong 256x256 (VAE 256/512 ch)
         if (cout % 256 != 0 && cout % 128 == 0 && mt * (cout / 128) >= 192) return {29, 1, nk};
     }
+    // 256x320: the ping-pong 16x16x32 kernel (tile 40, 5-12 % faster than the 32x32x16
+    // tile 25 on every conv / K >= 320 GEMM shape measured, scripts/gpu_tile_ab.sh) except
+    // for GEGLU, whose [16 h | 16 g] column pairs need 32-aligned per-wave column tiles
+    const int t256x320 = geglu ? 25 : 40;
     const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
-    if (t24 >= 192) return {25, 1, nk};
+    if (t24 >= 192) return {t256x320, 1, nk};
     if (nk >= 90 && t24 >= 64) {
         DmaPlan pl = plan_dma(M, cout, nk, geglu, 25, 0);
-        if (pl.id) return pl;
+        if (pl.id == 25) pl.id = t256x320;
+        return pl;
     }
     const long t7 = geglu ? ((M + 255) / 256) * ((cout + 127) / 128) : ((M + 127) / 128) * ((cout + 319) / 320);
     if (t7 >= 256) return {geglu ? 1 : 7, 1, nk};
@@ -854,6 +862,8 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     p.nkt = pl.nkt;
     switch (pl.id) {
         case 25: return run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s);   // 256x320, 8 waves of 64x160
+        case 40: return run_pp16<5>(p, ksize, cout, s);                // 256x320 ping-pong 16x16x32
+        case 41: return run_pp16<4>(p, ksize, cout, s);                // 256x256 ping-pong 16x16x32
         case 28: return run_m32<4, 2, 2, 4, 64, 2, 3>(p, ksize, cout, s);      // 256x256, 8 waves of 64x128
         case 29: return run_m32<4, 2, 2, 2, 64, 3, 3>(p, ksize, cout, s);      // 256x128, 8 waves of 64x64, 3 stages
         case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80

@@ -1,5 +1,6 @@
 """Per-shape timing of c2d_conv2d_igemm on the UNet's hot conv/GEMM shapes (N = 16)."""
 import math
+import os
 import sys
 from pathlib import Path
 
@@ -42,6 +43,22 @@ SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)
 ]
 
 
+def lib_gemm_us(m, kk, nn, iters=20):
+    """hipBLASLt (torch.mm) time of the equivalent plain GEMM [m, kk] x [kk, nn] fp16 -- the
+    im2col-free library ceiling for the same MACs (no conv addressing, no epilogue)."""
+    a = torch.randn(m, kk, device=dev, dtype=torch.float16)
+    b = torch.randn(kk, nn, device=dev, dtype=torch.float16)
+    for _ in range(3):
+        torch.mm(a, b)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        torch.mm(a, b)
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
 def run(name, k, h, cin, cout, act=None, n=N, iters=20):
     x = torch.randn(n, h, h, cin, device=dev, dtype=torch.float16)
     w = torch.randn(cout, cin, k, k, device=dev) / math.sqrt(k * k * cin)
@@ -62,7 +79,10 @@ def run(name, k, h, cin, cout, act=None, n=N, iters=20):
         r = ref.reshape(*ref.shape[:-1], -1, 2, 16)
         ref = (r[..., 0, :] * torch.nn.functional.gelu(r[..., 1, :])).reshape(*ref.shape[:-1], -1)
     err = ((out.float() - ref).norm() / ref.norm()).item()
-    print(f"{name:26s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  relerr {err:.1e}", flush=True)
+    hbm = 2.0 * (n * h * h * (cin + (cout // 2 if act == "geglu" else cout)) + cout * k * k * cin) / 5.0e6  # us at 5 TB/s
+    lib = lib_gemm_us(n * h * h, k * k * cin, cout) if os.environ.get("LIB", "1") == "1" else float("nan")
+    print(f"{name:26s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  hbm-floor {hbm:7.1f} us  hipblaslt-gemm {lib:7.1f} us "
+          f"({fl / lib / 1e6:7.1f} TF/s)  relerr {err:.1e}", flush=True)
 
 
 import os

@@ -1,0 +1,35 @@
+"""Summarise a rocprofv3 kernel_trace.csv: per (kernel, grid) totals and per family.
+usage: python scripts/kt_summary.py kernel_trace.csv [batches]"""
+import collections
+import csv
+import sys
+
+path = sys.argv[1]
+nb = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0
+agg = collections.defaultdict(lambda: [0, 0.0])
+fam = collections.defaultdict(float)
+
+
+def family(n):
+    for key, f in (("igemm_m32_kernel", "gemm32"), ("igemm_dma_kernel", "gemm16"), ("igemm_kernel", "gemm_reg"),
+                   ("splitk", "splitk"), ("attn_fwd", "attention"), ("attn_small", "attention"),
+                   ("window_attn", "attention"), ("gn_", "groupnorm"), ("ln_", "layernorm"),
+                   ("upsample", "upsample"), ("softmax", "softmax"), ("mel", "logmel")):
+        if key in n:
+            return f
+    return "other"
+
+
+for r in csv.DictReader(open(path)):
+    n = r["Kernel_Name"]
+    g = r.get("Grid_Size_X") or r.get("Grid_Size") or ""
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    agg[(n[:110], g)][0] += 1
+    agg[(n[:110], g)][1] += d
+    fam[family(n)] += d
+tot = sum(v[1] for v in agg.values())
+print(f"total {tot / 1e3:.1f} ms kernel time ({tot / 1e3 / nb:.1f} ms per batch over {nb:g} batches)")
+for f, v in sorted(fam.items(), key=lambda kv: -kv[1]):
+    print(f"  {f:10s} {v / 1e3 / nb:8.1f} ms/batch {100 * v / tot:5.1f}%")
+for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])[:70]:
+    print(f"{v[1] / 1e3:9.2f} ms {100 * v[1] / tot:5.1f}% {v[0]:6d} {v[1] / v[0]:9.1f}us grid={k[1]} {k[0]}")

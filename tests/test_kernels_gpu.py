@@ -128,7 +128,7 @@ def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
 
 # every tile configuration left in igemm.hip's kDmaTiles, forced through C2D_GEMM_TILE
 # (read per launch) and confirmed through c2d_conv2d_igemm_plan
-DMA_TILE_IDS = [25, 28, 29, 7, 1, 2, 3]
+DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3]
 
 
 @pytest.mark.parametrize("tile", DMA_TILE_IDS)
@@ -150,7 +150,7 @@ def test_every_dma_tile_forced(dev, monkeypatch, tile, k, split):
     close(nchw(out), ref)
 
 
-@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t != 7])   # 7 (odd column tiles) skips GEGLU
+@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 40)])   # odd column tiles: no GEGLU
 def test_every_dma_tile_forced_geglu(dev, monkeypatch, tile):
     m, cin, inner = 1024, 320, 640
     monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
