@@ -16,7 +16,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import check, lib, ptr, stream_ptr
+from . import torch_ops  # noqa: F401  (registers c2d::clap_log_mel)
 
 
 def _hz_to_mel_slaney(f):
@@ -100,9 +100,8 @@ class ClapLogMel:
         if out is None:
             out = torch.empty(b, self.frames, self.n_mels, device=self.device, dtype=torch.float32)
         assert out.shape == (b, self.frames, self.n_mels) and out.is_contiguous()
-        check(lib().c2d_clap_log_mel(ptr(wave), ptr(offsets), ptr(lengths), b, self.max_len, self.n_fft, self.hop,
-                                     ptr(self.window), ptr(self.filters), ptr(self.filter_range), self.n_mels,
-                                     ptr(out), stream_ptr()), "c2d_clap_log_mel")
+        torch.ops.c2d.clap_log_mel(wave, offsets, lengths, self.max_len, self.n_fft, self.hop, self.window,
+                                   self.filters, self.filter_range, self.n_mels, out)
         return out
 
 

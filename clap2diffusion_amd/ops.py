@@ -1,7 +1,9 @@
-"""Torch-facing wrappers over the C ABI (include/c2d.h).
+"""Torch-facing API over the C ABI (include/c2d.h), through the torch.library ops.
 
 Tensors are plain device buffers here: activations NHWC / row-major fp16,
-statistics fp32.  Every function launches on torch's current HIP stream, so
+statistics fp32.  Each function checks its operands, allocates the outputs and
+calls the registered ``torch.ops.c2d.*`` operator (clap2diffusion_amd.torch_ops),
+whose CUDA implementation launches the HIP kernel on torch's current stream, so
 the calls can be captured into a torch.cuda.CUDAGraph (hipGraph) as is.
 """
 from __future__ import annotations
@@ -11,7 +13,10 @@ import math
 
 import torch
 
-from ._lib import C2D_ACT, C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_NONE, C2D_PRO_SILU, ConvDesc, check, lib, ptr, stream_ptr
+from . import torch_ops  # noqa: F401  (registers the c2d:: operators)
+from ._lib import C2D_ACT
+
+C2D = torch.ops.c2d
 
 F16 = torch.float16
 
@@ -50,7 +55,7 @@ def pack_weights_device(w: torch.Tensor, cin_pad: int | None = None) -> tuple[to
     cp = max(cin_pad or cin, cin)
     kp = kpad_of(ks * ks * cp)
     out = torch.empty(cout, kp, device=w.device, dtype=F16)
-    check(lib().c2d_pack_weights(ptr(w), cout, cin, ks, cp, kp, ptr(out), stream_ptr()), "c2d_pack_weights")
+    C2D.pack_weights(w, cout, cin, ks, cp, kp, out)
     return out, kp
 
 
@@ -79,22 +84,19 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
          up: bool = False, x2: torch.Tensor | None = None, gn=None, gn_silu: bool = False, ln=None,
          silu_in: bool = False, act: str | None = None, temb: torch.Tensor | None = None,
          resid: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Implicit-GEMM conv / linear (c2d_conv2d_igemm).
+    """Implicit-GEMM conv / linear (c2d::conv2d_igemm).
 
     x: NHWC [N, H, W, C0] fp16 (or 2-D [M, C0] for a linear layer).
     gn: (scale, shift) fp32 [N, C0+C1]; ln: (stats [M, 2], gamma, beta).
     """
     _require(x, "x")
     if x.dim() == 2:
-        n, h, w = 1, 1, x.shape[0]
-        c0 = x.shape[1]
+        h, w = 1, x.shape[0]
     else:
-        n, h, w, c0 = x.shape
+        _, h, w, _ = x.shape
     assert x.is_contiguous() and x.dtype == F16
-    c1 = 0
     if x2 is not None:
         assert x2.is_contiguous() and x2.dtype == F16 and x2.shape[:-1] == x.shape[:-1]
-        c1 = x2.shape[-1]
     if ksize == 3:
         vh, vw = (2 * h, 2 * w) if up else (h, w)
         oh, ow = (vh + 2 - 3) // stride + 1, (vw + 2 - 3) // stride + 1
@@ -102,59 +104,29 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
         oh, ow = h, w
     out_cols = cout // 2 if act == "geglu" else cout
     if out is None:
-        shape = (n * oh * ow, out_cols) if x.dim() == 2 else (n, oh, ow, out_cols)
+        shape = (x.shape[0], out_cols) if x.dim() == 2 else (x.shape[0], oh, ow, out_cols)
         out = torch.empty(shape, device=x.device, dtype=F16)
-    d = ConvDesc()
-    d.src0 = ptr(x); d.src1 = ptr(x2); d.c0 = c0; d.c1 = c1
-    d.n, d.h, d.w, d.oh, d.ow = n, h, w, oh, ow
-    d.ksize, d.stride, d.up = ksize, stride, int(up)
-    d.weight = ptr(weight); d.cout = cout; d.kpad = kpad
-    if gn is not None:
-        d.pro = C2D_PRO_GN; d.pro_silu = int(gn_silu); d.pro_a = ptr(gn[0]); d.pro_b = ptr(gn[1])
-    elif ln is not None:
-        d.pro = C2D_PRO_LN; d.pro_a = ptr(ln[0]); d.gamma = ptr(ln[1]); d.beta = ptr(ln[2])
-    elif silu_in:
-        d.pro = C2D_PRO_SILU
-    else:
-        d.pro = C2D_PRO_NONE
-    d.bias = ptr(bias)
-    d.act = C2D_ACT[act]
-    if temb is not None:
-        d.temb = ptr(temb); d.temb_ld = temb.stride(0)
-    if resid is not None:
-        d.resid = ptr(resid); d.resid_ld = resid.stride(-2) if resid.dim() == 2 else resid.shape[-1]
-        assert resid.stride(-1) == 1
-    d.out = ptr(out)
-    d.out_ld = out.stride(-2) if out.dim() == 2 else out.shape[-1]
     assert out.stride(-1) == 1
-    wsb = lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
-    if wsb:
-        ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
-        d.ws = ptr(ws); d.ws_bytes = wsb
-    if _plan_probe is not None:
-        tid, ks = ctypes.c_int(), ctypes.c_int()
-        check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
-        _plan_probe.append((tid.value, ks.value))
-    check(lib().c2d_conv2d_igemm(ctypes.byref(d), stream_ptr()), "c2d_conv2d_igemm")
+    if resid is not None:
+        assert resid.stride(-1) == 1
+    gs, gh = gn if gn is not None else (None, None)
+    ls, lg, lb = ln if ln is not None else (None, None, None)
+    C2D.conv2d_igemm(x, weight, kpad, cout, ksize, stride, up, x2, gs, gh, gn_silu, ls, lg, lb, silu_in, bias,
+                     C2D_ACT[act], temb, resid, out)
     return out
 
 
-_plan_probe: list | None = None
-
-
 class record_conv_plans:
-    """Context manager collecting the (tile_id, ksplit) plan of every ops.conv call
+    """Context manager collecting the (tile_id, ksplit) plan of every conv call
     (c2d_conv2d_igemm_plan) -- lets tests assert which kernel configuration ran."""
 
     def __enter__(self):
-        global _plan_probe
         self.plans = []
-        _plan_probe = self.plans
+        torch_ops._plan_probe = self.plans
         return self.plans
 
     def __exit__(self, *exc):
-        global _plan_probe
-        _plan_probe = None
+        torch_ops._plan_probe = None
         return False
 
 
@@ -162,17 +134,10 @@ def group_norm_stats(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tens
                      x2: torch.Tensor | None = None):
     """-> (scale, shift) fp32 [N, C] folding GroupNorm(groups, eps) + affine."""
     _require(x, "x")
-    n = x.shape[0]
-    c0 = x.shape[-1]
-    c1 = x2.shape[-1] if x2 is not None else 0
-    hw = x.numel() // (n * c0)
-    c = c0 + c1
-    scale = torch.empty((n, c), device=x.device, dtype=torch.float32)
+    c = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    scale = torch.empty((x.shape[0], c), device=x.device, dtype=torch.float32)
     shift = torch.empty_like(scale)
-    ws = torch.empty(lib().c2d_groupnorm_workspace_size(n, c, hw) // 4, device=x.device, dtype=torch.float32)
-    rc = lib().c2d_groupnorm_stats(ptr(x), ptr(x2), c0, c1, n, hw, groups, eps, ptr(gamma), ptr(beta),
-                                   ptr(scale), ptr(shift), ptr(ws), stream_ptr())
-    check(rc, "c2d_groupnorm_stats")
+    C2D.groupnorm_stats(x, x2, groups, float(eps), gamma, beta, scale, shift)
     return scale, shift
 
 
@@ -180,53 +145,38 @@ def group_norm_apply(x: torch.Tensor, gn, silu: bool, x2: torch.Tensor | None = 
                      out: torch.Tensor | None = None) -> torch.Tensor:
     """Materialise act(GroupNorm(cat[x, x2])) from the folded (scale, shift) tables."""
     _require(x, "x")
-    n, c0 = x.shape[0], x.shape[-1]
-    c1 = x2.shape[-1] if x2 is not None else 0
-    hw = x.numel() // (n * c0)
+    c = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
     if out is None:
-        out = torch.empty((*x.shape[:-1], c0 + c1), device=x.device, dtype=F16)
-    rc = lib().c2d_groupnorm_apply(ptr(x), ptr(x2), c0, c1, n, hw, ptr(gn[0]), ptr(gn[1]), int(silu), ptr(out),
-                                   stream_ptr())
-    check(rc, "c2d_groupnorm_apply")
+        out = torch.empty((*x.shape[:-1], c), device=x.device, dtype=F16)
+    C2D.groupnorm_apply(x, x2, gn[0], gn[1], bool(silu), out)
     return out
 
 
 def group_norm(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor, silu: bool,
                x2: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """act(GroupNorm(cat[x, x2])) in one c2d_groupnorm call (single fused kernel for
+    """act(GroupNorm(cat[x, x2])) in one c2d::groupnorm call (single fused kernel for
     small images, stats + apply otherwise)."""
     _require(x, "x")
-    n, c0 = x.shape[0], x.shape[-1]
-    c1 = x2.shape[-1] if x2 is not None else 0
-    hw = x.numel() // (n * c0)
-    c = c0 + c1
+    c = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
     if out is None:
         out = torch.empty((*x.shape[:-1], c), device=x.device, dtype=F16)
-    wsb = lib().c2d_groupnorm_run_workspace_size(n, c, hw, groups)
-    ws = torch.empty((wsb + 15) // 16 * 4, device=x.device, dtype=torch.float32) if wsb else None
-    rc = lib().c2d_groupnorm(ptr(x), ptr(x2), c0, c1, n, hw, groups, eps, ptr(gamma), ptr(beta), int(silu),
-                             ptr(out), ptr(ws), wsb, stream_ptr())
-    check(rc, "c2d_groupnorm")
+    C2D.groupnorm(x, x2, groups, float(eps), gamma, beta, bool(silu), out)
     return out
 
 
 def layer_norm_stats(x2d: torch.Tensor, eps: float) -> torch.Tensor:
     _require(x2d, "x")
-    m, c = x2d.shape
-    st = torch.empty((m, 2), device=x2d.device, dtype=torch.float32)
-    check(lib().c2d_layernorm_stats(ptr(x2d), m, c, x2d.stride(0), eps, ptr(st), stream_ptr()), "c2d_layernorm_stats")
+    st = torch.empty((x2d.shape[0], 2), device=x2d.device, dtype=torch.float32)
+    C2D.layernorm_stats(x2d, float(eps), st)
     return st
 
 
 def layer_norm(x2d: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
                out: torch.Tensor | None = None) -> torch.Tensor:
     _require(x2d, "x")
-    m, c = x2d.shape
     if out is None:
-        out = torch.empty((m, c), device=x2d.device, dtype=F16)
-    rc = lib().c2d_layernorm(ptr(x2d), m, c, x2d.stride(0), eps, ptr(gamma), ptr(beta), ptr(out), out.stride(0),
-                             stream_ptr())
-    check(rc, "c2d_layernorm")
+        out = torch.empty(x2d.shape, device=x2d.device, dtype=F16)
+    C2D.layernorm(x2d, gamma, beta, float(eps), out)
     return out
 
 
@@ -241,44 +191,34 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, hea
         scale = 1.0 / math.sqrt(d)
     if out is None:
         out = torch.empty((batch * lq, heads * d), device=q.device, dtype=F16)
-    if key_bias is None:
-        rc = lib().c2d_attention_fwd(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-                                     out.stride(0), batch, heads, lq, lk, d, float(scale), 1, stream_ptr())
-        check(rc, "c2d_attention_fwd")
-        return out
-    kb = key_bias.to(device=q.device, dtype=torch.float32)
-    if kb.dim() != 3 or kb.shape[-1] != lk or kb.shape[0] not in (1, batch) or kb.shape[1] not in (1, heads):
-        raise ValueError(f"key_bias must be [batch|1, heads|1, {lk}], got {tuple(kb.shape)}")
-    kb = kb.contiguous()
-    ldb = kb.stride(0) if kb.shape[0] > 1 else 0
-    ldh = kb.stride(1) if kb.shape[1] > 1 else 0
-    rc = lib().c2d_attention_fwd_bias(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-                                      out.stride(0), batch, heads, lq, lk, d, float(scale), 1, ptr(kb), ldb, ldh,
-                                      stream_ptr())
-    check(rc, "c2d_attention_fwd_bias")
+    ldb = ldh = 0
+    kb = None
+    if key_bias is not None:
+        kb = key_bias.to(device=q.device, dtype=torch.float32)
+        if kb.dim() != 3 or kb.shape[-1] != lk or kb.shape[0] not in (1, batch) or kb.shape[1] not in (1, heads):
+            raise ValueError(f"key_bias must be [batch|1, heads|1, {lk}], got {tuple(kb.shape)}")
+        kb = kb.contiguous()
+        ldb = kb.stride(0) if kb.shape[0] > 1 else 0
+        ldh = kb.stride(1) if kb.shape[1] > 1 else 0
+    C2D.attention_fwd(q, k, v, batch, heads, lq, lk, d, float(scale), kb, ldb, ldh, out)
     return out
 
 
 def attention_small(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, heads: int, l: int, d: int,
                     causal: bool, scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Short-sequence (l <= 128, d = 64) attention, optionally causal (c2d_attention_small)."""
+    """Short-sequence (l <= 128, d = 64) attention, optionally causal (c2d::attention_small)."""
     _require(q, "q")
     if scale is None:
         scale = 1.0 / math.sqrt(d)
     if out is None:
         out = torch.empty((batch * l, heads * d), device=q.device, dtype=F16)
-    rc = lib().c2d_attention_small(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
-                                   out.stride(0), batch, heads, l, d, float(scale), int(causal), stream_ptr())
-    check(rc, "c2d_attention_small")
+    C2D.attention_small(q, k, v, batch, heads, l, d, float(scale), bool(causal), out)
     return out
 
 
 def window_attention(qkv: torch.Tensor, row_map: torch.Tensor, n_windows: int, heads: int, d: int,
                      bias: torch.Tensor, mask: torch.Tensor | None, out: torch.Tensor) -> torch.Tensor:
-    n_mask = mask.shape[0] if mask is not None else 0
-    rc = lib().c2d_window_attention(ptr(qkv), qkv.stride(0), ptr(row_map), n_windows, heads, d, ptr(bias), ptr(mask),
-                                    n_mask, ptr(out), out.stride(0), stream_ptr())
-    check(rc, "c2d_window_attention")
+    C2D.window_attention(qkv, row_map, n_windows, heads, d, bias, mask, out)
     return out
 
 
@@ -286,62 +226,53 @@ def htsat_mel_patches(mel: torch.Tensor, bn_scale: torch.Tensor, bn_shift: torch
     b, t, f = mel.shape
     assert f == 64 and mel.dtype == torch.float32 and mel.is_contiguous()
     out = torch.empty((b * 4096, 64), device=mel.device, dtype=F16)
-    check(lib().c2d_htsat_mel_patches(ptr(mel), b, t, ptr(bn_scale), ptr(bn_shift), ptr(out), stream_ptr()),
-          "c2d_htsat_mel_patches")
+    C2D.htsat_mel_patches(mel, bn_scale, bn_shift, out)
     return out
 
 
 def patch_merge_gather(x: torch.Tensor, b: int, h: int, w: int, c: int) -> torch.Tensor:
     out = torch.empty((b * (h // 2) * (w // 2), 4 * c), device=x.device, dtype=F16)
-    check(lib().c2d_patch_merge_gather(ptr(x), b, h, w, c, ptr(out), stream_ptr()), "c2d_patch_merge_gather")
+    C2D.patch_merge_gather(x, b, h, w, c, out)
     return out
 
 
 def row_mean(x: torch.Tensor, b: int, rows: int) -> torch.Tensor:
-    c = x.shape[1]
-    out = torch.empty((b, c), device=x.device, dtype=torch.float32)
-    check(lib().c2d_row_mean(ptr(x), b, rows, c, x.stride(0), ptr(out), stream_ptr()), "c2d_row_mean")
+    out = torch.empty((b, x.shape[1]), device=x.device, dtype=torch.float32)
+    C2D.row_mean(x, b, rows, out)
     return out
 
 
 def softmax_rows(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Row softmax of a 2-D fp16 matrix (c2d_softmax_rows); out may alias x."""
+    """Row softmax of a 2-D fp16 matrix (c2d::softmax_rows); out may alias x."""
     _require(x, "x")
     assert x.dim() == 2 and x.dtype == F16 and x.stride(1) == 1
     out = torch.empty_like(x) if out is None else out
     assert out.shape == x.shape and out.stride(1) == 1
-    check(lib().c2d_softmax_rows(ptr(x), x.shape[0], x.shape[1], x.stride(0), ptr(out), out.stride(0),
-                                 stream_ptr()), "c2d_softmax_rows")
+    C2D.softmax_rows(x, out)
     return out
 
 
 def l2_normalize_(x: torch.Tensor) -> torch.Tensor:
-    m, c = x.shape
-    check(lib().c2d_l2_normalize(ptr(x), m, c, stream_ptr()), "c2d_l2_normalize")
+    C2D.l2_normalize(x)
     return x
 
 
 def timestep_embedding(t_table: torch.Tensor, step_index: torch.Tensor | None, n: int, dim: int) -> torch.Tensor:
     out = torch.empty((n, dim), device=t_table.device, dtype=F16)
-    check(lib().c2d_timestep_embedding(ptr(t_table), ptr(step_index), n, dim, ptr(out), stream_ptr()),
-          "c2d_timestep_embedding")
+    C2D.timestep_embedding(t_table, step_index, n, dim, out)
     return out
 
 
 def cfg_ddim_step(eps: torch.Tensor, x: torch.Tensor, guidance: float, coef: torch.Tensor, step_index: torch.Tensor,
                   advance: bool = True) -> torch.Tensor:
-    b, c, hgt, wid = x.shape
-    rc = lib().c2d_cfg_ddim_step(ptr(eps), ptr(x), b, c, hgt * wid, float(guidance), ptr(coef), ptr(step_index),
-                                 int(advance), stream_ptr())
-    check(rc, "c2d_cfg_ddim_step")
+    C2D.cfg_ddim_step(eps, x, float(guidance), coef, step_index, bool(advance))
     return x
 
 
 def latent_to_nhwc(x: torch.Tensor, cpad: int, dup: bool) -> torch.Tensor:
     b, c, hgt, wid = x.shape
     out = torch.empty(((2 if dup else 1) * b, hgt, wid, cpad), device=x.device, dtype=F16)
-    check(lib().c2d_latent_to_nhwc(ptr(x), b, c, hgt * wid, cpad, int(dup), ptr(out), stream_ptr()),
-          "c2d_latent_to_nhwc")
+    C2D.latent_to_nhwc(x, cpad, bool(dup), out)
     return out
 
 
@@ -351,12 +282,12 @@ def upsample_nearest2x(x: torch.Tensor, out: torch.Tensor | None = None) -> torc
     x = x.contiguous()
     if out is None:
         out = torch.empty(n, 2 * h, 2 * w, c, device=x.device, dtype=x.dtype)
-    check(lib().c2d_upsample_nearest2x(ptr(x), n, h, w, c, ptr(out), stream_ptr()), "c2d_upsample_nearest2x")
+    C2D.upsample_nearest2x(x, out)
     return out
 
 
 def add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     if out is None:
         out = torch.empty_like(a)
-    check(lib().c2d_add(ptr(a), ptr(b), ptr(out), a.numel(), stream_ptr()), "c2d_add")
+    C2D.add(a, b, out)
     return out

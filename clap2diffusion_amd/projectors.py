@@ -183,10 +183,15 @@ class SoftHierarchicalDecomposition(nn.Module):
         logits = 10.0 * sim + self.gating_head(tokens)
         return torch.softmax(logits / self.temperature, dim=-1)
 
-    def forward(self, audio_features: torch.Tensor, return_stats: bool = False) -> Tuple[torch.Tensor, Dict]:
+    def tokens_and_assignments(self, audio_features: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """The forward's two tensors without the host-side info dict (no .item() sync:
+        capturable into a hipGraph)."""
         tokens = self.shared_mlp(audio_features).unsqueeze(1) + self.token_offsets.unsqueeze(0)
         assign = self.compute_assignments(tokens)
-        out = self.norm(self.cross_hierarchy_attn(tokens))
+        return self.norm(self.cross_hierarchy_attn(tokens)), assign
+
+    def forward(self, audio_features: torch.Tensor, return_stats: bool = False) -> Tuple[torch.Tensor, Dict]:
+        out, assign = self.tokens_and_assignments(audio_features)
         info = {"tokens": out, "assignments": assign, "temperature": self.temperature.item(),
                 "level_anchors": self.level_anchors}
         if return_stats:
@@ -338,6 +343,14 @@ class ImprovedHierarchicalAudioEncoder(nn.Module):
             losses["prior"] = torch.tensor(0.0, device=tokens.device)
         return losses
 
+    def routed_tokens(self, audio_features: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """forward(x, return_all=True)[1]["routed"] -- the level-keyed tokens the UNet's audio
+        processors consume -- without the projector-77 head, the losses and the stats
+        (no host syncs: capturable into a hipGraph).  Soft decomposition only."""
+        tokens_10, assignments = self.decomposer.tokens_and_assignments(audio_features)
+        hw = self.adaptive_weights(audio_features) if self.adaptive_weights is not None else None
+        return self.router(tokens_10, assignments, hw)
+
     def forward(self, audio_features: torch.Tensor, return_all: bool = False
                 ) -> Union[torch.Tensor, Tuple[torch.Tensor, Dict]]:
         if self.use_soft_decomposition:
@@ -381,9 +394,10 @@ class HierarchicalAudioV4(nn.Module):
 
 
 def normalize_tokens(audio_tokens: torch.Tensor, target_norm: float = 60.0) -> torch.Tensor:
-    """'Norm 60' rescale (scripts/inference.py:92-99): mean per-token L2 norm -> target."""
+    """'Norm 60' rescale (scripts/inference.py:92-99): mean per-token L2 norm -> target.
+    The reference's `if raw_norm > 0` is a device-side select here (same values, no host
+    sync, so the conditioning leg can be captured into a hipGraph)."""
     with torch.no_grad():
         raw = torch.norm(audio_tokens, dim=-1, keepdim=True).mean()
-        if raw > 0:
-            audio_tokens = audio_tokens * (target_norm / raw)
-    return audio_tokens
+        scale = torch.where(raw > 0, target_norm / raw, torch.ones_like(raw))
+        return audio_tokens * scale

@@ -105,3 +105,25 @@ def test_clap_encoder_checkpoint_is_loaded(dev, tmp_path):
     other = htsat_forward(W.synth_htsat(0), mel.cpu()[:, None].float())
     cos = torch.nn.functional.cosine_similarity(emb, ref).item()
     assert cos >= 0.999 and torch.nn.functional.cosine_similarity(emb, other).item() < 0.99
+
+
+def test_batch_graph_matches_eager_and_replays_new_inputs(pipe, dev):
+    # BatchGraph (conditioning, denoise steps and VAE as hipGraphs) == the eager-conditioning
+    # path, bit for bit, and a replay with new clips / prompts / latents follows them
+    import numpy as np
+    b, steps = 2, 6
+
+    def inputs(seeds, prompts):
+        clips = pipe.feature_extractor.crop([synthetic_thunder(s, 3.0 + s) for s in seeds])
+        wave = torch.from_numpy(np.concatenate(clips)).to(dev)
+        lens = torch.tensor([c.size for c in clips], dtype=torch.int32, device=dev)
+        offs = torch.tensor(np.cumsum([0] + [c.size for c in clips[:-1]]), dtype=torch.int64, device=dev)
+        ids = (tokenize([""] * b, dev), tokenize(prompts, dev))
+        return wave, offs, lens, ids, pipe.initial_latents(seeds)
+
+    for seeds, prompts in (([11, 12], ["a beach", "rain"]), ([13, 14], ["a forest", "thunder"])):
+        wave, offs, lens, ids, lat = inputs(seeds, prompts)
+        g = pipe.generate_batch_graphed(wave, offs, lens, ids, lat, steps, 7.5).clone()
+        e = pipe.generate_batch(pipe.feature_extractor.from_device(wave, offs, lens), None, steps, 7.5, ids=ids,
+                                latents=lat)
+        assert torch.equal(g, e)
