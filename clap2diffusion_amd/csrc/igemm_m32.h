@@ -18,10 +18,17 @@ namespace c2d {
 // conflict-free (each ds_read_b128 lane group of 16 hits 16 distinct slots):
 //   BK 64: chunk c of row r at slot c ^ ((r >> 1) & 7)
 //   BK 32: chunk c of row r at slot c ^ ((r >> 2) & 3)
-template <int BK>
+//   BK 32, SW 1 (16x16x32 fragment reads: lane l = row l & 15, chunk l >> 4): slot
+//   c ^ G[(r >> 2) & 3] with G = {0, 2, 3, 1}, conflict-free for that lane pattern
+template <int BK, int SW = 0>
+__device__ __forceinline__ int sw_of(int row) {
+    if (BK == 64) return (row >> 1) & 7;
+    if (SW == 1) return (0x78 >> (2 * ((row >> 2) & 3))) & 3;   // G = {0, 2, 3, 1} as 2-bit fields of 0x78
+    return (row >> 2) & 3;
+}
+template <int BK, int SW = 0>
 __device__ __forceinline__ int lds_sw(int row, int c) {
-    if (BK == 64) return row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
-    return row * 64 + ((c ^ ((row >> 2) & 3)) << 4);
+    return row * (2 * BK) + ((c ^ sw_of<BK, SW>(row)) << 4);
 }
 
 // LDS-DMA staging of one BK-deep K step of the A (im2col rows) and B (packed
@@ -32,7 +39,7 @@ __device__ __forceinline__ int lds_sw(int row, int c) {
 // instruction) covers RPP = 1024 / RB rows; the NA + NB pieces of a stage are
 // dealt round-robin to the NW waves, A first (NA % NW == 0, so piece slot i is
 // an A slot for i < NA / NW in every wave; the last B slot may be partial).
-template <int BM, int BN, int BK, int NW, int KS>
+template <int BM, int BN, int BK, int NW, int KS, int SW = 0>
 struct M32Loader {
     static constexpr int RB = 2 * BK, RPP = 1024 / RB, CPR = BK / 8;
     static constexpr int NA = BM / RPP, NB = BN / RPP;
@@ -54,9 +61,7 @@ struct M32Loader {
     }
     __device__ __forceinline__ int row_of(int wave, int i) const { return (wave + i * NW) * RPP + lrow; }
     // logical channel chunk this lane fetches so that the lane-linear image is swizzled (lds_sw)
-    __device__ __forceinline__ int chunk_of(int row) const {
-        return (BK == 64 ? (lchunk ^ ((row >> 1) & 7)) : (lchunk ^ ((row >> 2) & 3))) * 8;
-    }
+    __device__ __forceinline__ int chunk_of(int row) const { return (lchunk ^ sw_of<BK, SW>(row)) * 8; }
 
     __device__ __forceinline__ void init(const IgemmParams& p, int m0, int n0, int wave, int lane, int kb) {
         lrow = lane / CPR;

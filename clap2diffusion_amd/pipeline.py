@@ -182,10 +182,12 @@ class AudioToImageInference:
         """Per-sample CPU generator (seed) -> identical latents on any number of GPUs."""
         return initial_latents(seeds, self.height // 8, self.width // 8, self.device)
 
-    def denoiser(self, b: int, steps: int, guidance: float, ehs, audio_kwargs, latent_hw=None) -> GraphDenoiser:
-        """The captured-graph denoise loop for (batch, steps, guidance, latent size), built once."""
+    def denoiser(self, b: int, steps: int, guidance: float, ehs, audio_kwargs, latent_hw=None,
+                 slot: int = 0) -> GraphDenoiser:
+        """The captured-graph denoise loop for (batch, steps, guidance, latent size), built once;
+        `slot` keeps separate sampler states for batches run concurrently on different streams."""
         h, w = latent_hw or (self.height // 8, self.width // 8)
-        key = (b, steps, float(guidance), h, w)
+        key = (b, steps, float(guidance), h, w, slot)
         d = self._denoisers.get(key)
         if d is None:
             sch = DDIMScheduler()
@@ -234,18 +236,19 @@ class AudioToImageInference:
     @torch.no_grad()
     def generate_batch_graphed(self, wave: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
                                ids: tuple, latents: torch.Tensor, num_inference_steps: int = 50,
-                               guidance_scale: float = 7.5, use_hierarchical: bool = True) -> torch.Tensor:
+                               guidance_scale: float = 7.5, use_hierarchical: bool = True,
+                               slot: int = 0) -> torch.Tensor:
         """generate_batch from device-resident inputs (48 kHz clips concatenated + offsets /
         lengths, token ids, latents) as hipGraphs: one graph for the conditioning leg, the
         denoise-step graph replayed per DDIM step, one graph for the VAE decode (BatchGraph).
         The graphs are built on the first call for a given batch / steps / guidance / size and
         replayed afterwards with the new inputs copied into their static buffers."""
         key = (offsets.numel(), wave.numel(), num_inference_steps, float(guidance_scale), tuple(latents.shape),
-               bool(use_hierarchical))
+               bool(use_hierarchical), slot)
         bg = self._batch_graphs.get(key)
         if bg is None:
             bg = BatchGraph(self, wave, offsets, lengths, ids, latents, num_inference_steps, guidance_scale,
-                            use_hierarchical)
+                            use_hierarchical, slot)
             self._batch_graphs[key] = bg
         return bg.run(wave, offsets, lengths, ids, latents)
 
@@ -266,7 +269,7 @@ class BatchGraph:
     latents; all workspaces come from the graphs' private pools (allocated at capture)."""
 
     def __init__(self, pipe: AudioToImageInference, wave, offsets, lengths, ids, latents, steps: int,
-                 guidance: float, use_hierarchical: bool):
+                 guidance: float, use_hierarchical: bool, slot: int = 0):
         self.pipe, self.steps, self.use_hier = pipe, steps, use_hierarchical
         self.wave, self.offs, self.lens = wave.clone(), offsets.clone(), lengths.clone()
         self.ids_u, self.ids_c = ids[0].clone(), ids[1].clone()
@@ -277,7 +280,7 @@ class BatchGraph:
         # eager warm-up: builds (and captures) the denoiser, caches HTSAT tables, packs lazily
         ehs, kw, _ = pipe.condition(fe.from_device(self.wave, self.offs, self.lens, out=self.mel), self.ids_u,
                                     self.ids_c, use_hierarchical)
-        self.den = pipe.denoiser(b, steps, guidance, ehs, kw, latent_hw=tuple(self.lat.shape[-2:]))
+        self.den = pipe.denoiser(b, steps, guidance, ehs, kw, latent_hw=tuple(self.lat.shape[-2:]), slot=slot)
         self.den.ehs.copy_(ehs)
         self.den.prepare_context()
         if self.den.use_graph and self.den.graph is None:
