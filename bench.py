@@ -194,8 +194,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-configs", action="store_true", help="skip the c1/c2/c5 side measurements")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="split each GPU's batch into this many sub-batches run concurrently on separate HIP streams")
     a = ap.parse_args()
 
     from clap2diffusion_amd import distributed as D
@@ -216,35 +214,10 @@ def main():
     if ctx.rank == 0:
         log(f"[bench] setup {time.time() - t_setup:.1f}s, world={ctx.world}, batch/gpu={B}")
 
-    S = a.streams
-    assert B % S == 0, "--streams must divide the batch"
-    sub = B // S
-    sizes = [c.size for c in clips]
-    parts = []
-    for j in range(S):
-        lo = sum(sizes[: j * sub])
-        hi = sum(sizes[: (j + 1) * sub])
-        parts.append((wave[lo:hi], offs[j * sub:(j + 1) * sub] - lo, lens[j * sub:(j + 1) * sub],
-                      (inp.ids_uncond[j * sub:(j + 1) * sub], inp.ids_cond[j * sub:(j + 1) * sub]),
-                      inp.latents[j * sub:(j + 1) * sub]))
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(S - 1)]
-    img_all = torch.empty(B, a.res, a.res, 3, dtype=torch.uint8, device=dev)
-
     def one_batch():
-        # the whole batch as hipGraphs: conditioning leg, 50 denoise-step replays, VAE (BatchGraph);
-        # with --streams S, S sub-batches replay concurrently on S streams
-        if S == 1:
-            img = pipe.generate_batch_graphed(wave, offs, lens, (inp.ids_uncond, inp.ids_cond), inp.latents,
-                                              a.ddim_steps, 7.5)
-        else:
-            cur = torch.cuda.current_stream()
-            for j, (st, pt) in enumerate(zip(streams, parts)):
-                st.wait_stream(cur)
-                with torch.cuda.stream(st):
-                    img_all[j * sub:(j + 1) * sub].copy_(pipe.generate_batch_graphed(*pt, a.ddim_steps, 7.5, slot=j))
-            for st in streams[1:]:
-                cur.wait_stream(st)
-            img = img_all
+        # the whole batch as hipGraphs: conditioning leg, 50 denoise-step replays, VAE (BatchGraph)
+        img = pipe.generate_batch_graphed(wave, offs, lens, (inp.ids_uncond, inp.ids_cond), inp.latents,
+                                          a.ddim_steps, 7.5)
         ctx.all_gather(img, gathered)
         return img
 

@@ -48,6 +48,25 @@ template <int D> struct AttnCfg {
     static constexpr bool SUM_MFMA = DV > D;           // a spare V column carries the row sum
 };
 
+// Row max of a lane's 16 scores and its 3 partner lanes (l ^ 16, l ^ 32): two gfx950
+// lane-swap VALU ops instead of two ds_bpermute LDS round trips.  The file is built with
+// -fno-honor-nans (build.py): IEEE-mode fmaxf would prefix every MFMA-output operand with a
+// canonicalising v_max; without it the chain folds into v_max3 (inline asm v_max3 made the
+// compiler pad every asm statement with s_nop instead).
+__device__ __forceinline__ float quad_row_max(const f32x4 (&s)[4]) {
+    float m = s[0][0];
+#pragma unroll
+    for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m = fmaxf(m, s[kg][r]);
+    const unsigned u = __float_as_uint(m);
+    const auto x32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);   // {own, l ^ 32} per lane
+    const float m2 = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1]));
+    const unsigned u2 = __float_as_uint(m2);
+    const auto x16 = __builtin_amdgcn_permlane16_swap(u2, u2, false, false); // {own, l ^ 16} per lane
+    return fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
+}
+
 template <int D>
 __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B chunk ch of K row
     using C = AttnCfg<D>;
@@ -281,13 +300,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
         f16x8 pf[2][2];
 #pragma unroll
         for (int qg = 0; qg < 2; ++qg) {
-            float mx = s[qg][0][0];
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qg][kg][r]);
-            mx = fmaxf(mx, __shfl_xor(mx, 16));
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mx = quad_row_max(s[qg]);
             // lazy rescale: the running max only moves (and O, l get rescaled) when
             // some query of the wave gains more than 2^8; otherwise P <= 256 in fp16
             if (NEGC) {
