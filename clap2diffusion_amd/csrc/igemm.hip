@@ -18,6 +18,11 @@
 #include <stdlib.h>
 #include <type_traits>
 
+// 0 = A/B builds only: the 32x32 tiles 25 / 1 in place of the ping-pong 40 / 41 defaults
+#ifndef C2D_PP16_DEFAULT
+#define C2D_PP16_DEFAULT 1
+#endif
+
 namespace c2d {
 
 enum AMode { AM_1X1 = 0, AM_3X3_FAST = 1, AM_3X3_GEN = 2 };
@@ -838,13 +843,13 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     // 256 / 512 ch: 11-14 % faster)
     if (!geglu && cout % 320 != 0) {
         const long mt = (M + 255) / 256;
-        if (cout % 256 == 0 && mt * (cout / 256) >= 192) return {41, 1, nk};   // ping-pong 256x256 (VAE 256/512 ch)
+        if (C2D_PP16_DEFAULT && cout % 256 == 0 && mt * (cout / 256) >= 192) return {41, 1, nk};   // ping-pong 256x256 (VAE 256/512 ch)
         if (cout % 256 != 0 && cout % 128 == 0 && mt * (cout / 128) >= 192) return {29, 1, nk};
     }
     // 256x320: the ping-pong 16x16x32 kernel (tile 40, 5-12 % faster than the 32x32x16
     // tile 25 on every conv / K >= 320 GEMM shape measured, scripts/gpu_tile_ab.sh) except
     // for GEGLU, whose [16 h | 16 g] column pairs need 32-aligned per-wave column tiles
-    const int t256x320 = geglu ? 25 : 40;
+    const int t256x320 = (geglu || !C2D_PP16_DEFAULT) ? 25 : 40;
     const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
     if (t24 >= 192) return {t256x320, 1, nk};
     if (nk >= 90 && t24 >= 64) {

@@ -10,9 +10,20 @@ agg = collections.defaultdict(lambda: [0, 0.0])
 fam = collections.defaultdict(float)
 
 
+def _ks(n):
+    """KS template argument (1 = 1x1 GEMM, 3 = 3x3 conv) of the implicit-GEMM kernels."""
+    args = [a.strip() for a in n[n.index("<") + 1:n.index(">")].split(",")]
+    if "igemm_pp16_kernel" in n:
+        return args[1]
+    if "igemm_m32_kernel" in n:
+        return args[6]
+    return args[-1]
+
+
 def family(n):
-    for key, f in (("igemm_m32_kernel", "gemm32"), ("igemm_dma_kernel", "gemm16"), ("igemm_kernel", "gemm_reg"),
-                   ("splitk", "splitk"), ("attn_fwd", "attention"), ("attn_small", "attention"),
+    if "igemm_" in n and "<" in n and "igemm_kernel" not in n:
+        return "conv3x3" if _ks(n) == "3" else "gemm1x1"
+    for key, f in (("igemm_kernel", "gemm_reg"), ("splitk", "splitk"), ("attn_fwd", "attention"), ("attn_small", "attention"),
                    ("window_attn", "attention"), ("gn_", "groupnorm"), ("ln_", "layernorm"),
                    ("upsample", "upsample"), ("softmax", "softmax"), ("mel", "logmel")):
         if key in n:
