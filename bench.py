@@ -50,8 +50,13 @@ def measure_dominant_kernel(dev, iters: int = 20):
     b = torch.zeros(c, device=dev)
     res = torch.randn_like(x)
     out = torch.empty_like(x)
-    for _ in range(3):
+    with ops.record_conv_plans() as plans:
         ops.conv(x, wp, kp, c, ksize=3, bias=b, resid=res, out=out)
+    for _ in range(2):
+        ops.conv(x, wp, kp, c, ksize=3, bias=b, resid=res, out=out)
+    tile, split = plans[0]
+    kname = {40: "igemm_pp16_kernel<5,3> 256x320 ping-pong 16x16x32",
+             25: "igemm_m32_kernel 256x320 32x32x16"}.get(tile, f"tile {tile}")
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
@@ -64,8 +69,8 @@ def measure_dominant_kernel(dev, iters: int = 20):
     tflops = flop / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
-            "kernel": "c2d_conv2d_igemm (igemm_m32_kernel 256x320 tile) level-0 ResnetBlock2D conv 3x3 320->320 + residual, "
-                      "N=16 (CFG pair x 8 images) x 64x64",
+            "kernel": f"c2d_conv2d_igemm ({kname}, split {split}) level-0 ResnetBlock2D conv 3x3 320->320 + "
+                      "residual, N=16 (CFG pair x 8 images) x 64x64",
             "flop_per_launch": flop, "avg_us": round(ms * 1e3, 2)}
 
 
