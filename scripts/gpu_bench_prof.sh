@@ -15,4 +15,5 @@ P=/tmp/prof; rm -rf $P; mkdir -p $P
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/bench -o bench -- python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-pmc --no-configs > gpurun_out/prof/bench_stdout.log 2> gpurun_out/prof/bench_stderr.log || { echo "bench prof rc $?"; tail -20 gpurun_out/prof/bench_stderr.log; exit 1; }
 for f in $(find $P -name "*stats.csv"); do cp $f gpurun_out/prof/; done
 python3 scripts/kt_summary.py $(find $P -name "*kernel_trace.csv" | head -1) 2 > gpurun_out/prof/bench_by_kernel.txt
+gzip -c $(find $P -name "*kernel_trace.csv" | head -1) > gpurun_out/prof/bench_kernel_trace.csv.gz
 head -45 gpurun_out/prof/bench_by_kernel.txt

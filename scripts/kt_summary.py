@@ -39,6 +39,16 @@ for r in csv.DictReader(open(path)):
     agg[(n[:110], g)][1] += d
     fam[family(n)] += d
 tot = sum(v[1] for v in agg.values())
+# device idle between consecutive kernels (gaps under 100 us: launch / graph-node overhead,
+# not host pauses between phases)
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(path)))
+gap = 0.0
+end = iv[0][1] if iv else 0
+for a, b in iv[1:]:
+    if a > end and a - end < 100_000:
+        gap += (a - end) / 1e3
+    end = max(end, b)
+print(f"device idle between kernels (gaps < 100 us): {gap / 1e3 / nb:.1f} ms per batch")
 print(f"total {tot / 1e3:.1f} ms kernel time ({tot / 1e3 / nb:.1f} ms per batch over {nb:g} batches)")
 for f, v in sorted(fam.items(), key=lambda kv: -kv[1]):
     print(f"  {f:10s} {v / 1e3 / nb:8.1f} ms/batch {100 * v / tot:5.1f}%")
