@@ -75,8 +75,16 @@ def _read_wav(path: str) -> tuple[np.ndarray, int]:
 
 class AudioToImageInference:
     def __init__(self, checkpoint_dir="../checkpoints", device=None, seed: int = 0, height: int = 512,
-                 width: int = 512, use_graph: bool = True, verbose: bool = True):
+                 width: int = 512, use_graph: bool = True, verbose: bool = True, sd_model_path=None,
+                 clap_model_path=None):
+        """sd_model_path: a diffusers-format SD1.5 folder (unet/, vae/, text_encoder/);
+        clap_model_path: a ClapModel weights file or folder (e.g. laion/clap-htsat-unfused, the
+        model the reference loads at models/audio_encoder.py:47).  Without them the weights
+        are the seeded synthetic recipe (weights.py); checkpoint_dir/clap_encoder.pth and the
+        projector checkpoints load as in the reference."""
         self.checkpoint_dir = Path(checkpoint_dir)
+        self.sd_model_path = sd_model_path
+        self.clap_model_path = clap_model_path
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         if self.device.type != "cuda":
             raise RuntimeError("the sampling path runs on the HIP kernels only (MI355X); no CPU fallback")
@@ -96,8 +104,12 @@ class AudioToImageInference:
     def load_models(self):
         dev = self.device
         self._log(f"Initializing inference pipeline on {dev}")
+        sd15 = None
+        if self.sd_model_path:
+            self._log(f"Loading SD1.5 weights from {self.sd_model_path}")
+            sd15 = W.load_sd15_folder(self.sd_model_path)
         self.unet = UNet2DConditionModel().to(dev)
-        self.unet.load_diffusers_state_dict(W.synth_unet(self.seed))
+        self.unet.load_diffusers_state_dict(sd15["unet"] if sd15 else W.synth_unet(self.seed))
         self.manager = AudioProcessorManager(self.unet)
         self.manager.setup_processors(verbose=self.verbose)
         for level, p in self.manager.level_processors().items():
@@ -105,11 +117,16 @@ class AudioToImageInference:
             p.to(dev).eval()
         self.clap = HTSATEncoder().to(dev)
         clap_path = self.checkpoint_dir / "clap_encoder.pth"   # reference scripts/inference.py:38-41
+        if self.clap_model_path:
+            cp = Path(self.clap_model_path)
+            cp = W.find_weights_file(cp, ("model", "pytorch_model")) if cp.is_dir() else cp
+            self._log(f"Loading CLAP weights from {cp}")
+            self.clap.load_clap_state_dict(W.clap_audio_state_dict(W.load_weights_file(cp)))
         if clap_path.exists():
             self._log(f"Loading CLAP encoder from {clap_path}")
             self.clap.load_clap_state_dict(W.clap_audio_state_dict(
                 torch.load(clap_path, map_location="cpu", weights_only=True)))
-        else:
+        elif not self.clap_model_path:
             self.clap.load_clap_state_dict(W.synth_htsat(self.seed))
         self.hier_encoder = W.fill_module(ImprovedHierarchicalAudioEncoder(), "improved.", self.seed).to(dev).eval()
         adapter_path = self.checkpoint_dir / "audio_projector_stage2.pth"
@@ -124,9 +141,10 @@ class AudioToImageInference:
         if hpath.exists():
             self._log(f"Loading Hierarchical Model from {hpath}")
             self.hierarchical_model.load_state_dict(torch.load(hpath, map_location=dev, weights_only=True))
-        self.text_encoder = TextEncoder(dev, seed=self.seed)   # CLIPTextModel-keyed seeded weights
+        # CLIPTextModel-keyed weights: the SD1.5 text_encoder, else the seeded recipe
+        self.text_encoder = TextEncoder(dev, seed=self.seed, state_dict=sd15["text_encoder"] if sd15 else None)
         self.vae = VAEDecoder().to(dev)
-        self.vae.load_diffusers_state_dict(W.synth_vae_decoder(self.seed))
+        self.vae.load_diffusers_state_dict(sd15["vae"] if sd15 else W.synth_vae_decoder(self.seed))
         self.scheduler = DDIMScheduler()
         # the reference's ClapProcessor feature extraction (models/audio_encoder.py:163-167) on the GPU
         self.feature_extractor = ClapLogMel(dev)
@@ -332,8 +350,10 @@ def main():
     ap.add_argument("--cfg_scale", type=float, default=7.5, help="Guidance scale")
     ap.add_argument("--seed", type=int, default=None, help="Random seed")
     ap.add_argument("--no_hierarchical", action="store_true", help="Disable hierarchical processing")
+    ap.add_argument("--sd_model", type=str, default=None, help="diffusers-format SD1.5 folder (unet/, vae/, text_encoder/)")
+    ap.add_argument("--clap_model", type=str, default=None, help="ClapModel weights file or folder")
     a = ap.parse_args()
-    pipe = AudioToImageInference(checkpoint_dir=a.checkpoint_dir)
+    pipe = AudioToImageInference(checkpoint_dir=a.checkpoint_dir, sd_model_path=a.sd_model, clap_model_path=a.clap_model)
     img = pipe.generate(audio_path=a.audio, text_prompt=a.text, num_inference_steps=a.steps,
                         guidance_scale=a.cfg_scale, seed=a.seed, use_hierarchical=not a.no_hierarchical)
     img.save(a.output)

@@ -319,6 +319,61 @@ def clap_audio_state_dict(ck: dict) -> "OrderedDict[str, torch.Tensor]":
     return out
 
 
+# ------------------------------------------------------------------ checkpoint files
+def load_weights_file(path) -> dict:
+    """A state dict from a .safetensors file (safetensors loader) or a torch .bin / .pt /
+    .pth file (torch.load with weights_only=True: nothing in the file is executed)."""
+    path = str(path)
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path)
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
+def find_weights_file(folder, stems=("diffusion_pytorch_model", "model", "pytorch_model")):
+    """The first <stem>.safetensors / <stem>.bin present in a diffusers / transformers folder."""
+    from pathlib import Path
+    folder = Path(folder)
+    for stem in stems:
+        for ext in (".safetensors", ".bin"):
+            f = folder / (stem + ext)
+            if f.exists():
+                return f
+    raise FileNotFoundError(f"no {'/'.join(stems)}.safetensors|.bin under {folder}")
+
+
+# diffusers < 0.14 VAE attention names (what the SD1.5 vae/ files carry) -> current ones
+_VAE_OLD_ATTN = {"query": "to_q", "key": "to_k", "value": "to_v", "proj_attn": "to_out.0"}
+
+
+def vae_decoder_state_dict(sd: dict) -> "OrderedDict[str, torch.Tensor]":
+    """Decoder half of an AutoencoderKL state dict (decoder.*, post_quant_conv.*), with the
+    old mid-block attention names renamed and their 1x1-conv weights flattened to Linear."""
+    out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    for k, v in sd.items():
+        if not (k.startswith("decoder.") or k.startswith("post_quant_conv.")):
+            continue
+        parts = k.split(".")
+        if "attentions" in parts and len(parts) >= 2 and parts[-2] in _VAE_OLD_ATTN:
+            k = ".".join(parts[:-2] + [_VAE_OLD_ATTN[parts[-2]], parts[-1]])
+            if v.dim() == 4:
+                v = v[:, :, 0, 0]
+        out[k] = v
+    if "post_quant_conv.weight" not in out:
+        raise KeyError("no AutoencoderKL decoder keys (decoder.* / post_quant_conv.*) in checkpoint")
+    return out
+
+
+def load_sd15_folder(folder) -> dict:
+    """SD1.5 weights from a diffusers-format folder (unet/, vae/, text_encoder/, each a
+    *.safetensors or *.bin): {"unet": ..., "vae": decoder keys, "text_encoder": ...}."""
+    from pathlib import Path
+    folder = Path(folder)
+    return {"unet": load_weights_file(find_weights_file(folder / "unet")),
+            "vae": vae_decoder_state_dict(load_weights_file(find_weights_file(folder / "vae"))),
+            "text_encoder": load_weights_file(find_weights_file(folder / "text_encoder", ("model", "pytorch_model")))}
+
+
 # ------------------------------------------------------------------ CLIP text tower
 CLIP_TEXT_CFG = dict(vocab=49408, width=768, layers=12, heads=12, mlp=3072, max_len=77)
 

@@ -127,3 +127,35 @@ def test_batch_graph_matches_eager_and_replays_new_inputs(pipe, dev):
         e = pipe.generate_batch(pipe.feature_extractor.from_device(wave, offs, lens), None, steps, 7.5, ids=ids,
                                 latents=lat)
         assert torch.equal(g, e)
+
+
+@pytest.mark.timeout(900)
+def test_sd15_folder_weights_drive_the_pipeline(dev, tmp_path):
+    # a diffusers-format SD1.5 folder (unet/ + vae/ with the pre-0.14 attention names and the
+    # encoder half + text_encoder/) holding the seed-7 recipe: images identical to the
+    # pipeline that synthesises the same weights in memory
+    from safetensors.torch import save_file
+    from clap2diffusion_amd import weights as W
+    (tmp_path / "unet").mkdir()
+    save_file(W.synth_unet(7), str(tmp_path / "unet" / "diffusion_pytorch_model.safetensors"))
+    vae = {}
+    old = {"to_q": "query", "to_k": "key", "to_v": "value", "to_out.0": "proj_attn"}
+    for k, v in W.synth_vae_decoder(7).items():
+        for new, o in old.items():
+            if f"attentions.0.{new}." in k:
+                k = k.replace(new, o)
+                v = v[:, :, None, None] if v.dim() == 2 else v
+        vae[k] = v
+    vae["encoder.conv_in.weight"] = torch.zeros(128, 3, 3, 3)
+    (tmp_path / "vae").mkdir()
+    save_file(vae, str(tmp_path / "vae" / "diffusion_pytorch_model.safetensors"))
+    (tmp_path / "text_encoder").mkdir()
+    save_file(dict(W.synth_clip_text(7)), str(tmp_path / "text_encoder" / "model.safetensors"))
+    a = AudioToImageInference(device=dev, seed=7, height=128, width=128, verbose=False, sd_model_path=tmp_path)
+    b = AudioToImageInference(device=dev, seed=7, height=128, width=128, verbose=False)
+    mel = a.mel_features([synthetic_thunder(1)])
+    ids = (tokenize([""], dev), tokenize(["a beach"], dev))
+    lat = a.initial_latents([1])
+    ia = a.generate_batch(mel, None, 5, 7.5, ids=ids, latents=lat).cpu()
+    ib = b.generate_batch(mel, None, 5, 7.5, ids=ids, latents=lat).cpu()
+    assert (ia.int() - ib.int()).abs().max().item() <= 1

@@ -26,3 +26,30 @@ def test_clap_checkpoint_forms(tmp_path):
         torch.save(ck, p)
         got = W.clap_audio_state_dict(torch.load(p, map_location="cpu", weights_only=True))
         assert set(got) == set(sd) and all(torch.equal(got[k], sd[k]) for k in sd)
+
+
+def test_weights_files_and_sd15_folder(tmp_path):
+    """diffusers-folder loading: safetensors and .bin files, the AutoencoderKL decoder half with
+    the pre-0.14 attention names (query/key/value/proj_attn, 1x1-conv shaped) renamed."""
+    from safetensors.torch import save_file
+    g = torch.Generator().manual_seed(0)
+    unet = {"conv_in.weight": torch.randn(320, 4, 3, 3, generator=g), "conv_in.bias": torch.randn(320, generator=g)}
+    a = "decoder.mid_block.attentions.0."
+    vae = {"encoder.conv_in.weight": torch.randn(2, 2), "quant_conv.weight": torch.randn(8, 8, 1, 1),
+           "post_quant_conv.weight": torch.randn(4, 4, 1, 1), "post_quant_conv.bias": torch.randn(4),
+           a + "query.weight": torch.randn(512, 512, generator=g), a + "query.bias": torch.randn(512),
+           a + "proj_attn.weight": torch.randn(512, 512, 1, 1, generator=g), a + "group_norm.weight": torch.ones(512)}
+    text = {"text_model.final_layer_norm.weight": torch.ones(768)}
+    for sub, sd, name in (("unet", unet, "diffusion_pytorch_model.safetensors"),
+                          ("vae", vae, "diffusion_pytorch_model.safetensors")):
+        (tmp_path / sub).mkdir()
+        save_file(sd, str(tmp_path / sub / name))
+    (tmp_path / "text_encoder").mkdir()
+    torch.save(text, tmp_path / "text_encoder" / "pytorch_model.bin")
+    out = W.load_sd15_folder(tmp_path)
+    assert set(out["unet"]) == set(unet) and torch.equal(out["unet"]["conv_in.weight"], unet["conv_in.weight"])
+    assert set(out["vae"]) == {"post_quant_conv.weight", "post_quant_conv.bias", a + "to_q.weight", a + "to_q.bias",
+                               a + "to_out.0.weight", a + "group_norm.weight"}
+    assert out["vae"][a + "to_out.0.weight"].shape == (512, 512)
+    assert torch.equal(out["vae"][a + "to_out.0.weight"], vae[a + "proj_attn.weight"][:, :, 0, 0])
+    assert torch.equal(out["text_encoder"]["text_model.final_layer_norm.weight"], torch.ones(768))
