@@ -1,0 +1,137 @@
+// Host-side checks of the C ABI under AddressSanitizer (tests/test_asan_cpu.py builds this
+// against a --cuda-host-only -fsanitize=address build of the library sources: no device code
+// is embedded and nothing is launched).  Covers the planner / workspace queries over every
+// UNet / VAE / HTSAT / CLIP conv and GEMM shape plus a deterministic random sweep, and the
+// argument-validation paths of the compute entry points (which must return a negative
+// C2D_E_* code before touching the GPU).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "c2d.h"
+
+static int fails = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            ++fails;                                                          \
+        }                                                                     \
+    } while (0)
+
+static const int kTiles[] = {0, 1, 2, 3, 7, 25, 28, 29, 40, 41};
+
+static c2d_conv_desc desc(int n, int h, int w, int c0, int c1, int ksize, int stride, int cout, int act) {
+    static char dummy[64] __attribute__((aligned(16)));
+    c2d_conv_desc d;
+    std::memset(&d, 0, sizeof d);
+    d.src0 = dummy;
+    d.src1 = c1 ? dummy : nullptr;
+    d.c0 = c0;
+    d.c1 = c1;
+    d.n = n;
+    d.h = h;
+    d.w = w;
+    d.ksize = ksize;
+    d.stride = stride;
+    d.oh = ksize == 3 ? (h + 2 - 3) / stride + 1 : h;
+    d.ow = ksize == 3 ? (w + 2 - 3) / stride + 1 : w;
+    d.weight = dummy;
+    d.cout = cout;
+    d.kpad = (ksize * ksize * (c0 + c1) + 63) / 64 * 64;
+    d.act = act;
+    d.out = dummy;
+    d.out_ld = act == C2D_ACT_GEGLU ? cout / 2 : cout;
+    return d;
+}
+
+static void check_plan(const c2d_conv_desc& d0) {
+    c2d_conv_desc d = d0;
+    int tile = -1, split = -1;
+    const size_t ws = c2d_conv2d_igemm_workspace_size(&d);
+    CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK);   // no workspace: never split
+    bool known = false;
+    for (int t : kTiles) known |= t == tile;
+    CHECK(known);
+    CHECK(split == 1);
+    if (ws) {
+        std::vector<char> buf(ws + 16);
+        d.ws = reinterpret_cast<void*>((reinterpret_cast<uintptr_t>(buf.data()) + 15) & ~uintptr_t(15));
+        d.ws_bytes = ws;
+        CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK);
+        CHECK(split > 1);
+        const size_t m = (size_t)d.n * d.oh * d.ow;
+        CHECK(ws >= (size_t)split * m * d.cout * sizeof(float));
+        d.ws_bytes = ws - 4;   // one short: the plan must fall back to one slice
+        CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK);
+        CHECK(split == 1);
+    }
+}
+
+int main() {
+    // ---- planner over the model shapes (CFG batches of 2 and 16 images)
+    const int unet[][4] = {{64, 320, 320, 3},   {64, 960, 320, 3},   {64, 640, 320, 3},  {32, 320, 640, 3},
+                           {32, 640, 640, 3},   {32, 1920, 640, 3},  {32, 1280, 640, 3}, {16, 640, 1280, 3},
+                           {16, 1280, 1280, 3}, {16, 2560, 1280, 3}, {8, 1280, 1280, 3}, {8, 2560, 1280, 3},
+                           {64, 320, 960, 1},   {64, 320, 320, 1},   {64, 1280, 320, 1}, {32, 640, 1920, 1},
+                           {32, 2560, 640, 1},  {16, 1280, 3840, 1}, {16, 5120, 1280, 1}, {64, 8, 320, 3}};
+    for (int nb : {2, 16})
+        for (auto& s : unet) {
+            check_plan(desc(nb, s[0], s[0], s[1], 0, s[3], 1, s[2], C2D_ACT_NONE));
+            if (s[3] == 1 && s[2] % 320 == 0)
+                check_plan(desc(nb, s[0], s[0], s[1], 0, 1, 1, 8 * s[1], C2D_ACT_GEGLU));
+        }
+    check_plan(desc(16, 64, 64, 640, 320, 3, 1, 320, C2D_ACT_NONE));   // up-block skip concat
+    check_plan(desc(16, 64, 64, 320, 0, 3, 2, 320, C2D_ACT_NONE));     // stride-2 downsample
+    for (int nb : {1, 2, 8})                                            // VAE decoder
+        for (int hw : {64, 128, 256, 512})
+            for (int c : {128, 256, 512}) check_plan(desc(nb, hw, hw, c, 0, 3, 1, c, C2D_ACT_NONE));
+    check_plan(desc(1, 1, 4096, 96, 0, 1, 1, 288, C2D_ACT_NONE));       // HTSAT stage-0 QKV (rows as width)
+    check_plan(desc(1, 1, 154, 768, 0, 1, 1, 3072, C2D_ACT_QUICK_GELU)); // CLIP MLP
+
+    // ---- deterministic random sweep
+    unsigned s = 12345;
+    auto rnd = [&](int lo, int hi) { s = s * 1103515245u + 12345u; return lo + (int)((s >> 8) % (unsigned)(hi - lo + 1)); };
+    for (int i = 0; i < 3000; ++i) {
+        const int ks = rnd(0, 1) ? 3 : 1;
+        const int c0 = 64 * rnd(1, 40), c1 = rnd(0, 3) == 0 ? 64 * rnd(1, 20) : 0;
+        const int geglu = ks == 1 && c1 == 0 && rnd(0, 4) == 0;
+        const int cout = geglu ? 32 * rnd(1, 200) : 4 * rnd(1, 1000);
+        const int hw = rnd(1, 96);
+        check_plan(desc(rnd(1, 16), hw, rnd(1, 96), c0, c1, ks, ks == 3 && rnd(0, 5) == 0 ? 2 : 1, cout,
+                        geglu ? C2D_ACT_GEGLU : C2D_ACT_NONE));
+    }
+
+    // ---- validation paths: nothing may be launched
+    c2d_conv_desc d = desc(2, 8, 8, 320, 0, 3, 1, 320, C2D_ACT_NONE);
+    {
+        c2d_conv_desc e = d; e.src0 = nullptr;            CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_ARG);
+        e = d; e.ksize = 2;                               CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        e = d; e.c0 = 321;                                CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        e = d; e.kpad = 64;                               CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        e = d; e.cout = 322;                              CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        e = d; e.c1 = 64;                                 CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_ARG);
+        e = d; e.act = C2D_ACT_GEGLU; e.cout = 336;       CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        CHECK(c2d_conv2d_igemm(nullptr, nullptr) == C2D_E_ARG);
+        int t, sp;
+        CHECK(c2d_conv2d_igemm_plan(nullptr, &t, &sp) == C2D_E_ARG);
+        CHECK(c2d_conv2d_igemm_workspace_size(nullptr) == 0);
+    }
+    static char buf[1 << 12] __attribute__((aligned(16)));
+    CHECK(c2d_attention_fwd(nullptr, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_ARG);
+    CHECK(c2d_attention_fwd(buf, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 48, 0.1f, 1, nullptr) == C2D_E_SHAPE);
+    CHECK(c2d_attention_fwd(buf, 41, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_ALIGN);
+    CHECK(c2d_attention_fwd(buf + 2, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_ALIGN);
+    CHECK(c2d_attention_fwd(buf, 40, buf, 40, buf, 40, buf, 40, 0, 1, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_SHAPE);
+    CHECK(c2d_attention_fwd(buf, 40, buf, 40, buf, 40, buf, 40, 1, 2, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_SHAPE);
+    CHECK(c2d_groupnorm_workspace_size(16, 320, 4096) > 0);
+    CHECK(c2d_version() != nullptr && std::strlen(c2d_version()) > 0);
+
+    if (fails) {
+        std::fprintf(stderr, "%d check(s) failed\n", fails);
+        return 1;
+    }
+    std::printf("abi_host_check: ok\n");
+    return 0;
+}
