@@ -39,16 +39,6 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
         for (int i = 0; i < 8; ++i) { sum[q][i] = 0.f; sq[q][i] = 0.f; shift[q][i] = 0.f; }
 
     if (active) {
-#pragma unroll
-        for (int q = 0; q < CPT; ++q) {
-            const int ch = ch_base + q * 256;
-            if (ch >= nch) continue;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                int c = ch * 8 + i;
-                shift[q][i] = gn_read(s0, s1, c0, c1, img, (c / cpg) * cpg);
-            }
-        }
         auto ld8 = [&](int pix, int q) {
             const size_t gp = img + pix;
             const int c = (ch_base + q * 256) * 8;
@@ -63,23 +53,47 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
                 sq[q][i] += d * d;
             }
         };
-        // four pixels per trip, all loads issued before the sums (same per-thread pixel
+        // UN pixels per trip, all loads issued before the sums (same per-thread pixel
         // order as one at a time, so the statistics are bit-identical); chunk 0 always
-        // exists for an active thread, so CPT = 1 has no per-load branch
+        // exists for an active thread, so CPT = 1 has no per-load branch.  A block owns
+        // ~64 rows, i.e. ~11 per thread at 320 channels: eight per trip (not four) halves
+        // the HBM round trips of these short-lived blocks, and the first trip's loads are
+        // in flight while the per-group shifts load
+        constexpr int UN = CPT == 1 ? 8 : 4;
         int pix = p_begin + r0;
-        for (; pix + 3 * R < p_end; pix += 4 * R) {
-            f16x8 v[4][CPT];
+        bool first = true;
+        for (; pix + (UN - 1) * R < p_end; pix += UN * R) {
+            f16x8 v[UN][CPT];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < UN; ++u)
 #pragma unroll
                 for (int q = 0; q < CPT; ++q)
                     if (q == 0 || ch_base + q * 256 < nch) v[u][q] = ld8(pix + u * R, q);
+            if (first) {
+#pragma unroll
+                for (int q = 0; q < CPT; ++q) {
+                    const int ch = ch_base + q * 256;
+                    if (ch >= nch) continue;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) shift[q][i] = gn_read(s0, s1, c0, c1, img, ((ch * 8 + i) / cpg) * cpg);
+                }
+                first = false;
+            }
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < UN; ++u)
 #pragma unroll
                 for (int q = 0; q < CPT; ++q)
                     if (q == 0 || ch_base + q * 256 < nch) acc8(v[u][q], q);
+        }
+        if (first) {
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                const int ch = ch_base + q * 256;
+                if (ch >= nch) continue;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) shift[q][i] = gn_read(s0, s1, c0, c1, img, ((ch * 8 + i) / cpg) * cpg);
+            }
         }
         for (; pix < p_end; pix += R) {
 #pragma unroll
