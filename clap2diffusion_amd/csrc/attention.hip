@@ -89,8 +89,8 @@ __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B
 // key-padding form diffusers builds: fp32 kbias[b * kb_ldb + h * kb_ldh + key], natural-
 // log units, added to q.k * scale before the softmax); only with NEGC = false, where s
 // holds the unscaled q.k, so the bias enters as bias / scale.
-template <int D, bool MASK, bool NEGC, bool RES = false, bool KBIAS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 64 ? ATTN_WPE : 1)))
+template <int D, bool MASK, bool NEGC, bool RES = false, bool KBIAS = false, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(D <= 64 ? ATTN_WPE : 1)))
 attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
@@ -99,6 +99,8 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int kb_ldh = 0, float kb_mul = 0.f) {
     static_assert(!(KBIAS && NEGC), "key bias only on the fma-softmax form");
     using C = AttnCfg<D>;
+    constexpr int NT = 64 * NWV;                              // threads; NWV waves x 32 queries per block
+    constexpr int NLD = (64 * C::DCH + NT - 1) / NT;          // staged K / V chunks per thread per tile
     constexpr int SLOT = C::K_BYTES + C::V_BYTES;
     constexpr int NSLOT = RES ? 2 : 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -117,13 +119,13 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     // zero the K padding columns once (never rewritten) and the V pad columns
 #pragma unroll
     for (int sl = 0; sl < NSLOT; ++sl) {
-        for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 256) {
+        for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += NT) {
             int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
             *reinterpret_cast<f16x8*>(Ks + sl * SLOT + k_off<D>(row, ch)) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
         }
         // V pad columns: zeros, except column D = 1.0 when there is one, so the PV
         // product also accumulates the softmax row sum (SUM_MFMA)
-        for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 256) {
+        for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += NT) {
             int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
             f16x8 z = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
             if (ch == C::DCH) z[0] = (f16)1.0f;
@@ -133,16 +135,16 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
 
     const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
     const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
-    f16x8 rk[C::NLD], rv[C::NLD];
+    f16x8 rk[NLD], rv[NLD];
     auto gload = [&](int t) {
 #pragma unroll
-        for (int i = 0; i < C::NLD; ++i) {
-            const int idx = tid + 256 * i;
+        for (int i = 0; i < NLD; ++i) {
+            const int idx = tid + NT * i;
             const int row = idx / C::DCH, ch = idx - row * C::DCH;
             // keys past lk re-read the last key: their scores are masked to -inf,
             // so their V rows meet P = 0
             const int key = min(t * 64 + row, lk - 1);
-            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
+            if (NT * i < 64 * C::DCH - (NT - 1) || idx < 64 * C::DCH) {
                 rk[i] = *reinterpret_cast<const f16x8*>(kbase + (size_t)key * ldk + ch * 8);
                 rv[i] = *reinterpret_cast<const f16x8*>(vbase + (size_t)key * ldv + ch * 8);
             }
@@ -150,9 +152,9 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     };
     auto swrite = [&](int sl) {
 #pragma unroll
-        for (int i = 0; i < C::NLD; ++i) {
-            const int idx = tid + 256 * i;
-            if (256 * i < 64 * C::DCH - 255 || idx < 64 * C::DCH) {
+        for (int i = 0; i < NLD; ++i) {
+            const int idx = tid + NT * i;
+            if (NT * i < 64 * C::DCH - (NT - 1) || idx < 64 * C::DCH) {
                 const int row = idx / C::DCH, ch = idx - row * C::DCH;
                 *reinterpret_cast<f16x8*>(Ks + sl * SLOT + k_off<D>(row, ch)) = rk[i];
                 *reinterpret_cast<f16x8*>(Vs + sl * SLOT + row * C::VS + ch * 16) = rv[i];
@@ -179,7 +181,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
 
     const int qb_end = RES ? min(nqb, (qgrp + 1) * qpb_) : qgrp + 1;
     for (int qb = qgrp * qpb_; qb < qb_end; ++qb) {
-    const int q0 = qb * 128 + wave * 32;
+    const int q0 = qb * (32 * NWV) + wave * 32;
 
     // Q fragments (B operand of S^T = K Q^T): query q0 + 16 qg + li, d = 32 dc + 8 g .. +7;
     // tail (16x16x16): d = 32 NDC + 4 g .. +3
@@ -728,6 +730,12 @@ static bool attn_res() {   // C2D_ATTN_RES=0: stream K/V tiles for short key seq
     return v != 0;
 }
 
+static bool attn_w8() {   // C2D_ATTN_W8=1: 8-wave blocks for the d = 40 self-attention (A/B)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_ATTN_W8"); v = e ? atoi(e) : 1; }
+    return v != 0;
+}
+
 static int attn_pipelined() {
     static int v = -1;
     if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
@@ -803,6 +811,17 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
     hipLaunchKernelGGL((attn_fwd_kernel<D, MASK, NEGC>), grid, dim3(256), smem, s, (const f16*)q, ldq, (const f16*)k, \
                        ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb, \
                        attn_abl())
+    if constexpr (D == 40) {
+        // 8-wave blocks (256 queries): one K / V staging chunk per thread instead of two
+        // (L0: 586-628 -> 560-594 us, same box); d = 80 measured 72 -> 76 us with them
+        if (lk % 64 == 0 && lk >= 256 && attn_negc() && attn_w8()) {
+            const int nqb8 = (lq + 255) / 256;
+            hipLaunchKernelGGL((attn_fwd_kernel<D, false, true, false, false, 8>), dim3(nqb8 * batch * heads),
+                               dim3(512), smem, s, (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o,
+                               ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb8, attn_abl());
+            return check_launch();
+        }
+    }
     // NEGC pays its Q pre-scale and peeled first tile back only over several key tiles
     // (measured: 4096 keys d = 40 681 -> 646 us, d = 80 75.7 -> 72.6; 77 keys 35.8 -> 38.4)
     const bool mask = lk % 64 != 0, negc = attn_negc() && lk >= 256;
