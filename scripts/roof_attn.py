@@ -11,7 +11,10 @@ import torch  # noqa: E402
 from clap2diffusion_amd import ops  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-b, h, l, d = 16, 8, 4096, 40
+# [iters] [L] [images]: the c5 shape (768^2, 96^2 latent, B = 4 -> 8 CFG images) is "5 9216 8"
+l = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+b = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+h, d = 8, 40
 dev = torch.device("cuda:0")
 qkv = torch.randn(b * l, 3 * h * d, device=dev, dtype=torch.float16)
 c = h * d
