@@ -53,12 +53,15 @@ template <int D> struct AttnCfg {
 // -fno-honor-nans (build.py): IEEE-mode fmaxf would prefix every MFMA-output operand with a
 // canonicalising v_max; without it the chain folds into v_max3 (inline asm v_max3 made the
 // compiler pad every asm statement with s_nop instead).
-__device__ __forceinline__ float quad_row_max(const f32x4 (&s)[4]) {
+__device__ __forceinline__ float lane_max16(const f32x4 (&s)[4]) {
     float m = s[0][0];
 #pragma unroll
     for (int kg = 0; kg < 4; ++kg)
 #pragma unroll
         for (int r = 0; r < 4; ++r) m = fmaxf(m, s[kg][r]);
+    return m;
+}
+__device__ __forceinline__ float quad_max(float m) {   // max over lanes l, l ^ 16, l ^ 32, l ^ 48
     const unsigned u = __float_as_uint(m);
     const auto x32 = __builtin_amdgcn_permlane32_swap(u, u, false, false);   // {own, l ^ 32} per lane
     const float m2 = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1]));
@@ -302,13 +305,16 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
         f16x8 pf[2][2];
 #pragma unroll
         for (int qg = 0; qg < 2; ++qg) {
-            const float mx = quad_row_max(s[qg]);
             // lazy rescale: the running max only moves (and O, l get rescaled) when
             // some query of the wave gains more than 2^8; otherwise P <= 256 in fp16
             if (NEGC) {
                 // s already holds log2-domain scores minus m_run; the first tile rebases
-                // m_run (0 so far) to the tile max, later ones only move it up
-                if (t == 0 || __builtin_amdgcn_ballot_w64(mx > 8.0f)) {
+                // m_run (0 so far) to the tile max, later ones only move it up.  Whether any
+                // row max exceeds 8 is decided on the lane maxima (same ballot); the row max
+                // itself (two lane swaps) is formed only when a rescale happens
+                const float lmx = lane_max16(s[qg]);
+                if (t == 0 || __builtin_amdgcn_ballot_w64(lmx > 8.0f)) {
+                    const float mx = quad_max(lmx);
                     const float delta = t == 0 ? mx : fmaxf(mx, 0.f);
                     const float alpha = __builtin_amdgcn_exp2f(-delta);
                     m_run[qg] += delta;
@@ -320,6 +326,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                     for (int kg = 0; kg < 4; ++kg) s[qg][kg] -= delta;
                 }
             } else {
+                const float mx = quad_max(lane_max16(s[qg]));
                 const float m_cand = fmaxf(m_run[qg], mx * scale_log2);
                 if (__builtin_amdgcn_ballot_w64(m_cand > m_run[qg] + 8.0f)) {
                     const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_cand);
