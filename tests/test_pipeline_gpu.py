@@ -91,6 +91,23 @@ def test_c1_workload_512_10_steps_from_waveform(pipe, dev):
     assert p >= 30.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
 
 
+@pytest.mark.timeout(900)
+def test_c5_shape_768_from_waveform(pipe, dev):
+    # BASELINE.json c5's shape (768^2 = 96^2 latent: 9216-key self-attention, 48^2 / 24^2 / 12^2
+    # levels) end to end from the waveform, 3 DDIM steps (the oracle UNet at 96^2 takes ~10 s
+    # per CFG-pair call): PSNR >= 30 dB, mean |diff| <= 3/255
+    wave = synthetic_thunder(4)
+    mel = pipe.mel_features([wave])
+    ids = (tokenize([""], dev), tokenize(["a thunderstorm"], dev))
+    lat = initial_latents([4], 96, 96, dev)
+    img = pipe.generate_batch(mel, None, 3, 7.5, ids=ids, latents=lat).cpu()
+    assert img.shape == (1, 768, 768, 3)
+    ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 3)
+    p = psnr(img, ref)
+    mad = (img.float() - ref.float()).abs().mean().item()
+    assert p >= 30.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+
+
 def test_clap_encoder_checkpoint_is_loaded(dev, tmp_path):
     # reference scripts/inference.py:38-41: clap_encoder.pth in checkpoint_dir drives the CLAP
     # tower (here a CLAPAudioEncoder-style state dict, keys under "clap_model.")
