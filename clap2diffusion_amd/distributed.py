@@ -73,6 +73,12 @@ class DPContext:
             return [t]
         if out is None:
             out = [torch.empty_like(t) for _ in range(self.world)]
+        if self.backend == "gloo" and t.is_cuda:   # rehearsal path: gloo gathers host copies
+            host = [torch.empty_like(t, device="cpu") for _ in range(self.world)]
+            dist.all_gather(host, t.contiguous().cpu())
+            for o, h in zip(out, host):
+                o.copy_(h)
+            return out
         dist.all_gather(out, t.contiguous())
         return out
 
@@ -90,15 +96,17 @@ class DPContext:
 
 def init(device_type: str = "cuda", backend: str | None = None) -> DPContext:
     """Read the launcher environment; for world > 1 bind this process to its GPU
-    (LOCAL_RANK) and join the process group ("nccl" = RCCL for cuda, "gloo" for cpu)."""
+    (LOCAL_RANK) and join the process group ("nccl" = RCCL for cuda, "gloo" for cpu).
+    Rehearsal knobs (a one-GPU box running several ranks): C2D_DP_ONE_DEVICE=1 puts every
+    rank on cuda:0, C2D_DP_BACKEND=gloo replaces RCCL (which needs one GPU per rank)."""
     rank, ws, local = world()
     if device_type == "cuda":
-        dev = torch.device("cuda", local)
+        dev = torch.device("cuda", 0 if os.environ.get("C2D_DP_ONE_DEVICE") == "1" else local)
         if ws > 1:
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if device_type == "cuda" else "gloo")
+    be = backend or os.environ.get("C2D_DP_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if ws > 1 and not dist.is_initialized():
         if be == "nccl":
             dist.init_process_group(be, device_id=dev)
