@@ -21,6 +21,10 @@ LIB = PKG / "libc2d_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip", "audio.hip"]
+# compile units: igemm.hip once per kernel family (C2D_IGEMM_PART, see its header) so
+# the families build in parallel; (source, extra defines, object stem)
+UNITS = [("igemm.hip", (f"C2D_IGEMM_PART={k}",), f"igemm_p{k}") for k in range(4)] + \
+        [(s, (), Path(s).stem) for s in SOURCES[1:]]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I", str(ROOT / "include")]
 # attention rescales its MFMA accumulators with VALU every tile: keep them in
@@ -32,7 +36,7 @@ EXTRA = {"attention.hip": ["-Xarch_device", "-mllvm=-amdgpu-mfma-vgpr-form=true"
 
 def _digest(defines=()) -> str:
     h = hashlib.sha256()
-    h.update(repr((FLAGS, EXTRA, tuple(defines))).encode())
+    h.update(repr((FLAGS, EXTRA, tuple(defines), UNITS)).encode())
     for f in sorted(CSRC.iterdir()):
         if f.suffix in (".hip", ".h", ".cpp"):
             h.update(f.name.encode())
@@ -42,9 +46,11 @@ def _digest(defines=()) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src: str, build_dir: Path, defines=()) -> Path:
-    obj = build_dir / (Path(src).stem + ".o")
-    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], *EXTRA.get(src, []), "-c", str(CSRC / src), "-o", str(obj)]
+def _compile(unit, build_dir: Path, defines=()) -> Path:
+    src, udefs, stem = unit
+    obj = build_dir / (stem + ".o")
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in (*defines, *udefs)], *EXTRA.get(src, []), "-c", str(CSRC / src),
+           "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -66,7 +72,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bo
     build_dir = ROOT / "build" / ("c2d_abl" if ablation else "c2d")
     build_dir.mkdir(parents=True, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, build_dir, defines), SOURCES))
+        objs = list(ex.map(lambda u: _compile(u, build_dir, defines), UNITS))
     tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)

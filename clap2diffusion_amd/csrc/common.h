@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <type_traits>
 #include "../../include/c2d.h"
 
 typedef _Float16 f16;
@@ -30,6 +31,17 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 
 namespace c2d {
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).  For loops whose
+// body is too large for the unroller (which then leaves an accumulator array indexed
+// by a run-time counter, i.e. in scratch memory): here every index is a constant.
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 
 // thread-local last launch error, exposed as c2d_last_hip_error()
 extern thread_local int g_last_hip_error;

@@ -23,6 +23,15 @@
 #define C2D_PP16_DEFAULT 1
 #endif
 
+// The library compiles this file once per kernel family (build.py: -DC2D_IGEMM_PART=k)
+// so the families build in parallel: 0 = host API, planner, register-staged kernels and
+// the split-K combine; 1 = ping-pong 16x16x32 tiles; 2 = 32x32x16 tiles; 3 = 16x16x32
+// LDS-DMA tiles.  Undefined (-1) = everything in one object.
+#ifndef C2D_IGEMM_PART
+#define C2D_IGEMM_PART -1
+#endif
+#define C2D_PART(k) (C2D_IGEMM_PART < 0 || C2D_IGEMM_PART == (k))
+
 namespace c2d {
 
 enum AMode { AM_1X1 = 0, AM_3X3_FAST = 1, AM_3X3_GEN = 2 };
@@ -603,31 +612,32 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         }
         return;
     }
-    // LDS-staged epilogue (epilogue.h): accumulators -> fp32 image of up to 32 rows
-    // per wave, then one compact loop of coalesced 16-B chunks
+    // LDS-staged epilogue (epilogue.h): passes of up to 32 rows of fp32 per wave image,
+    // the bias added as the accumulators are written
     __syncthreads();
     {
         constexpr int PITCHF = TN * 16 + 4;
         constexpr int RB = TM < 2 ? TM : 2;                  // 16-row tiles per image
         float* img = reinterpret_cast<float*>(smem) + wave * 16 * RB * PITCHF;
         const int mw0 = m0 + wm * TM * 16, nw0 = n0 + wn * TN * 16;
+        static_for<0, TM / RB>([&](auto pass) __attribute__((always_inline)) {
+            constexpr int b0 = RB * decltype(pass)::value;
+            epi_pass<RB * 16, TN * 16, false>(p, img, PITCHF, mw0 + b0 * 16, nw0, lane, [&]() __attribute__((always_inline)) {
+                f32x4 bv[TN];   // per pass (an L1 hit after the first): fewer registers held across passes
 #pragma unroll
-        for (int b0 = 0; b0 < TM; b0 += RB) {
+                for (int a = 0; a < TN; ++a) bv[a] = bias4(p, nw0 + a * 16 + 4 * (lane >> 4));
 #pragma unroll
-            for (int bb = 0; bb < RB; ++bb)
+                for (int bb = 0; bb < RB; ++bb)
 #pragma unroll
-                for (int a = 0; a < TN; ++a)
-                    *reinterpret_cast<f32x4*>(img + (bb * 16 + (lane & 15)) * PITCHF + a * 16 + 4 * (lane >> 4)) =
-                        acc[a][b0 + bb];
-            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
-            __builtin_amdgcn_wave_barrier();
-            epi_rows<RB * 16, TN * 16>(p, img, PITCHF, mw0 + b0 * 16, nw0, lane);
-            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
-            __builtin_amdgcn_wave_barrier();
-        }
+                    for (int a = 0; a < TN; ++a)
+                        *reinterpret_cast<f32x4*>(img + (bb * 16 + (lane & 15)) * PITCHF + a * 16 + 4 * (lane >> 4)) =
+                            acc[a][b0 + bb] + bv[a];
+            });
+        });
     }
 }
 
+#if C2D_PART(0)
 // split-K combine + epilogue: out[m, j..j+3] = act(sum_s ws[s][m][j..] + bias) + temb + resid
 // (same operation order as epilogue_tiles; slices summed in fixed order)
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
@@ -663,6 +673,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
         *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
     }
 }
+#else
+__global__ void splitk_reduce_kernel(IgemmParams p);
+#endif
 
 }  // namespace c2d
 #include "igemm_m32.h"
@@ -727,6 +740,30 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     else launch_dma<WM, WN, TM, TN, ST, 3>(p, s);
 }
 
+// One wrapper per DMA tile id, each compiled in its kernel family's part.
+#define C2D_TILE_FN(ID) void run_tile_##ID(IgemmParams& p, int ksize, int cout, hipStream_t s)
+namespace c2d {
+C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
+C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3);
+#if C2D_PART(1)
+C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
+C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
+#endif
+#if C2D_PART(2)
+C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
+C2D_TILE_FN(28) { run_m32<4, 2, 2, 4, 64, 2, 3>(p, ksize, cout, s); }            // 256x256, 8 waves of 64x128
+C2D_TILE_FN(29) { run_m32<4, 2, 2, 2, 64, 3, 3>(p, ksize, cout, s); }            // 256x128, 8 waves of 64x64, 3 stages
+#endif
+#if C2D_PART(3)
+C2D_TILE_FN(7) { run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s); }   // 128x320, 8 waves of 64x80
+C2D_TILE_FN(1) { run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s); }   // 256x128, 8 waves of 64x64
+C2D_TILE_FN(2) { run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s); }   // 128x128, 4 waves of 64x64
+C2D_TILE_FN(3) { run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s); }   // 64x64, 4 waves of 32x32
+#endif
+}  // namespace c2d
+#undef C2D_TILE_FN
+
+#if C2D_PART(0)
 // Tile / split-K choice from a cost model: estimated time = rounds of resident
 // blocks x per-block time (K steps + a fill/epilogue overhead, at the per-CU
 // rate measured on gfx950 for that tile with the CU full) + the split-K combine
@@ -737,7 +774,7 @@ struct DmaTile { int id, bm, bn, occ; float rate; bool geglu; };
 static const DmaTile kDmaTiles[] = {
     // 32x32x16 MFMA, LDS-DMA ring (igemm_m32.h); rate 0 = chosen by the rules in plan_for only
     {25, 256, 320, 1, 0.0f, true},
-    {40, 256, 320, 1, 0.0f, false},   // ping-pong 16x16x32 (80-column wave tiles: no GEGLU pairs)
+    {40, 256, 320, 1, 0.0f, false},   // ping-pong 16x16x32 (80-column wave tiles: no GEGLU pairs in the plain epilogue)
     {41, 256, 256, 1, 0.0f, true},
     {28, 256, 256, 1, 0.0f, true},
     {29, 256, 128, 1, 0.0f, true},
@@ -848,7 +885,8 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     }
     // 256x320: the ping-pong 16x16x32 kernel (tile 40, 5-12 % faster than the 32x32x16
     // tile 25 on every conv / K >= 320 GEMM shape measured, scripts/gpu_tile_ab.sh) except
-    // for GEGLU, whose [16 h | 16 g] column pairs need 32-aligned per-wave column tiles
+    // for GEGLU, whose [16 h | 16 g] column pairs need 32-aligned per-wave column tiles in
+    // the plain (per-wave image) epilogue
     const int t256x320 = (geglu || !C2D_PP16_DEFAULT) ? 25 : 40;
     const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
     if (t24 >= 192) return {t256x320, 1, nk};
@@ -866,15 +904,15 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
     switch (pl.id) {
-        case 25: return run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s);   // 256x320, 8 waves of 64x160
-        case 40: return run_pp16<5>(p, ksize, cout, s);                // 256x320 ping-pong 16x16x32
-        case 41: return run_pp16<4>(p, ksize, cout, s);                // 256x256 ping-pong 16x16x32
-        case 28: return run_m32<4, 2, 2, 4, 64, 2, 3>(p, ksize, cout, s);      // 256x256, 8 waves of 64x128
-        case 29: return run_m32<4, 2, 2, 2, 64, 3, 3>(p, ksize, cout, s);      // 256x128, 8 waves of 64x64, 3 stages
-        case 7: return run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s);   // 128x320, 8 waves of 64x80
-        case 1: return run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s);   // 256x128, 8 waves of 64x64
-        case 2: return run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s);   // 128x128, 4 waves of 64x64
-        default: return run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s);  // 64x64, 4 waves of 32x32
+        case 25: return run_tile_25(p, ksize, cout, s);
+        case 40: return run_tile_40(p, ksize, cout, s);
+        case 41: return run_tile_41(p, ksize, cout, s);
+        case 28: return run_tile_28(p, ksize, cout, s);
+        case 29: return run_tile_29(p, ksize, cout, s);
+        case 7: return run_tile_7(p, ksize, cout, s);
+        case 1: return run_tile_1(p, ksize, cout, s);
+        case 2: return run_tile_2(p, ksize, cout, s);
+        default: return run_tile_3(p, ksize, cout, s);
     }
 }
 
@@ -995,3 +1033,5 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     }
     return check_launch();
 }
+
+#endif  // C2D_PART(0)

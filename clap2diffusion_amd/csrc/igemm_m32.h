@@ -188,7 +188,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 
 // LDS-staged epilogue for the 32x32 layout (workgroup LDS free; caller
 // synchronised): accumulators -> fp32 LDS image (tiny unrolled code), then
-// epi_rows (epilogue.h) for bias / activation / GEGLU / temb / residual.
+// epi_pass (epilogue.h) for activation / GEGLU / temb / residual (bias added here).
 // Column groups of <= 3 tiles of 32 keep the per-wave image at 32 x 96 fp32.
 template <int TM, int TN>
 __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x16 (&acc)[TN][TM], int mw0, int nw0,
@@ -197,27 +197,47 @@ __device__ __forceinline__ void epilogue32_lds(const IgemmParams& p, const f32x1
     constexpr int PITCHF = G * 32 + 4;                        // fp32 row pitch (+16 B)
     float* img = reinterpret_cast<float*>(lds) + wave * 32 * PITCHF;
     const int lr = lane & 31, lh = lane >> 5;
+    if (!p.resid && !p.temb) {   // plain outputs (GEGLU, QKV): the round-1 loop (epi_rows_plain)
 #pragma unroll
-    for (int b = 0; b < TM; ++b) {
+        for (int b = 0; b < TM; ++b) {
 #pragma unroll
-        for (int a0 = 0; a0 < TN; a0 += G) {
+            for (int a0 = 0; a0 < TN; a0 += G) {
 #pragma unroll
-            for (int a = a0; a < a0 + G && a < TN; ++a)
+                for (int a = a0; a < a0 + G && a < TN; ++a)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+                        *reinterpret_cast<f32x4*>(img + lr * PITCHF + (a - a0) * 32 + g * 8 + lh * 4) = v;
+                    }
+                __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
+                __builtin_amdgcn_wave_barrier();
+                const int nt = (a0 + G <= TN) ? G : TN - a0;   // folds per unrolled group
+                if (nt == 3) epi_rows_plain<32, 96>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
+                else if (nt == 2) epi_rows_plain<32, 64>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
+                else epi_rows_plain<32, 32>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
+                __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        return;
+    }
+    static_for<0, TM * ((TN + G - 1) / G)>([&](auto pass) __attribute__((always_inline)) {
+        constexpr int b = decltype(pass)::value / ((TN + G - 1) / G);
+        constexpr int a0 = (decltype(pass)::value % ((TN + G - 1) / G)) * G;
+        constexpr int nt = (a0 + G <= TN) ? G : TN - a0;   // column tiles in this group
+        // bias-added accumulators of column tiles a0 .. a0 + nt - 1 -> the wave's image
+        auto write_img = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int a = a0; a < a0 + nt; ++a)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
+                    const f32x4 bv = bias4(p, nw0 + a * 32 + g * 8 + lh * 4);
                     const f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
-                    *reinterpret_cast<f32x4*>(img + lr * PITCHF + (a - a0) * 32 + g * 8 + lh * 4) = v;
+                    *reinterpret_cast<f32x4*>(img + lr * PITCHF + (a - a0) * 32 + g * 8 + lh * 4) = v + bv;
                 }
-            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
-            __builtin_amdgcn_wave_barrier();
-            const int nt = (a0 + G <= TN) ? G : TN - a0;   // folds per unrolled group
-            if (nt == 3) epi_rows<32, 96>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
-            else if (nt == 2) epi_rows<32, 64>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
-            else epi_rows<32, 32>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane);
-            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
+        };
+        epi_pass<32, nt * 32, true>(p, img, PITCHF, mw0 + b * 32, nw0 + a0 * 32, lane, write_img);
+    });
 }
 
 // Direct epilogue from the accumulators (no LDS round trip), the activation fixed

@@ -1,5 +1,5 @@
 // Ping-pong implicit GEMM on v_mfma_f32_16x16x32_f16 (included by igemm.hip after
-// igemm_m32.h; uses IgemmParams, M32Loader, lds_sw, wait_vm*, epi_rows, splitk_reduce).
+// igemm_m32.h; uses IgemmParams, M32Loader, lds_sw, wait_vm*, epi_pass, splitk_reduce).
 //
 // Structure (cdna_hip_programming.md §5, "the 256² 8-phase template", adapted to the
 // implicit-GEMM conv and a 256 x 320 tile):
@@ -135,9 +135,14 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
         }
         return;
     }
-    // LDS-staged epilogue (epilogue.h): 32 rows (two 16-row tiles) of fp32 per wave image
+    // LDS-staged epilogue (epilogue.h).  Outputs with a residual or a time embedding: four
+    // passes; in each every wave writes 32 of its rows (bias added) into one workgroup image
+    // of 2 x 32 rows x the tile's 16 TN x 4 columns and all 512 threads finish it, each
+    // chunk's residual / temb loads issued with its image read (one wait per chunk; the
+    // round-1 per-chunk branches paid up to three serialised round trips).  Plain outputs:
+    // the round-1 per-wave image loop (faster there, see epi_rows_plain).
     __syncthreads();
-    {
+    if (!p.resid && !p.temb) {
         constexpr int PITCHF = TN * 16 + 4;
         float* img = reinterpret_cast<float*>(smem) + wave * 32 * PITCHF;
 #pragma unroll
@@ -150,17 +155,36 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
                         acc[a][b0 + bb];
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
             __builtin_amdgcn_wave_barrier();
-            epi_rows<32, TN * 16>(p, img, PITCHF, mw0 + b0 * 16, nw0, lane);
+            epi_rows_plain<32, TN * 16>(p, img, PITCHF, mw0 + b0 * 16, nw0, lane);
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
             __builtin_amdgcn_wave_barrier();
         }
+    } else {
+        constexpr int BN = 4 * TN * 16, PITCHB = BN + 4;
+        float* img = reinterpret_cast<float*>(smem);
+        const int wr0 = wr * 32, wc0 = wc * TN * 16;
+        static_for<0, TMW / 2>([&](auto pass) __attribute__((always_inline)) {
+            constexpr int b0 = 2 * decltype(pass)::value;
+            epi_pass<64, BN, true, 512, TMW * 16>(p, img, PITCHB, m0 + b0 * 16, n0, tid, [&]() __attribute__((always_inline)) {
+                f32x4 bv[TN];
+#pragma unroll
+                for (int a = 0; a < TN; ++a) bv[a] = bias4(p, nw0 + a * 16 + 4 * (lane >> 4));
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                    for (int a = 0; a < TN; ++a)
+                        *reinterpret_cast<f32x4*>(img + (wr0 + bb * 16 + (lane & 15)) * PITCHB + wc0 + a * 16 +
+                                                  4 * (lane >> 4)) = acc[a][b0 + bb] + bv[a];
+            });
+        });
     }
 }
 
 template <int TN, int KS>
 static void launch_pp16(const IgemmParams& p, hipStream_t s) {
     constexpr int ring = 2 * (256 + 4 * TN * 16) * 128;
-    constexpr int epi = 8 * 32 * (TN * 16 + 4) * 4;
+    constexpr int epi_wg = 64 * (4 * TN * 16 + 4) * 4, epi_wv = 8 * 32 * (TN * 16 + 4) * 4;   // epilogue images
+    constexpr int epi = epi_wg > epi_wv ? epi_wg : epi_wv;
     constexpr int smem = ring > epi ? ring : epi;
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     auto k = igemm_pp16_kernel<TN, KS>;
