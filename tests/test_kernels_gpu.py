@@ -150,6 +150,40 @@ def test_every_dma_tile_forced(dev, monkeypatch, tile, k, split):
     close(nchw(out), ref)
 
 
+@pytest.mark.parametrize("tile", DMA_TILE_IDS)
+@pytest.mark.parametrize("cout,temb,resid,bias", [
+    (336, True, True, True),     # 16-B (W = 8) form, every operand, ragged last column tile
+    (332, True, True, True),     # 8-B (W = 4) generic form (cout % 8 != 0)
+    (320, False, True, False),   # residual without a bias (zero bias in the image write)
+    (320, True, False, True),    # time embedding alone
+])
+def test_epilogue_operand_forms(dev, monkeypatch, tile, cout, temb, resid, bias):
+    """The epilogue forms (epilogue.h: workgroup image on the ping-pong tiles, per-wave
+    prefetch on the 16x16 DMA family, compact / plain loops) on a ragged M (2 x 13 x 17
+    pixels: partial row tiles, rows straddling images) against torch fp32."""
+    n, h, w_, cin = 2, 13, 17, 320
+    monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
+    monkeypatch.setenv("C2D_GEMM_SPLIT", "1")
+    x = gen(n, cin, h, w_, seed=111)
+    w = gen(cout, cin, 3, 3, seed=112, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=113) if bias else None
+    te = gen(n, cout, seed=114) if temb else None
+    r = gen(n, cout, h, w_, seed=115) if resid else None
+    ref = F.conv2d(x, w, b, padding=1)
+    if te is not None:
+        ref = ref + te[:, :, None, None]
+    if r is not None:
+        ref = ref + r
+    wp, kp = ops.pack_conv_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(nhwc(x).half().to(dev), wp.to(dev), kp, cout, ksize=3,
+                       bias=b.float().to(dev) if b is not None else None,
+                       temb=te.half().to(dev) if te is not None else None,
+                       resid=nhwc(r).half().to(dev) if r is not None else None)
+    assert plans == [(tile, 1)], plans
+    close(nchw(out), ref)
+
+
 @pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 40)])   # odd column tiles: no GEGLU
 def test_every_dma_tile_forced_geglu(dev, monkeypatch, tile):
     m, cin, inner = 1024, 320, 640
