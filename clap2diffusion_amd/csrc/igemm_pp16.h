@@ -27,6 +27,10 @@
 // DVFS item 7: ~1.12-1.15x the FLOP/s on random data).
 #pragma once
 
+#ifndef C2D_PP16_LGKM_ALL
+#define C2D_PP16_LGKM_ALL 1   // 0: lgkmcnt(0) only in phase 3 (measured neutral: bench 7.845 / 7.840 vs 7.850 / 7.837)
+#endif
+
 namespace c2d {
 
 // Accumulators stay in the VGPR form the compiler picks.  AGPR accumulators overlap LDS
@@ -97,7 +101,12 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
                     if (q * PPH + i < P) ld.piece(st, Wn, wave, q * PPH + i);
             }
             if (q == 3 && nxt) wait_vm_c<0>();   // own pieces of K step kt+1 landed
-            __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
+            // lgkmcnt(0) before the barrier only where the WAR argument needs it (the last
+            // reads of this ring slot, phase 3); in phases 0-2 the fragment reads' latency
+            // runs under the barrier wait and the compiler's own wait before the first MFMA
+            // that uses them (cdna_hip_programming.md 8-phase template: wait after the barrier)
+            if (q == 3 || C2D_PP16_LGKM_ALL)
+                __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
             C2D_BAR();
             // ---- MFMA section
             if (C2D_ABL(p.abl, 2)) {   // timing ablation: fragments kept live, no MFMA
