@@ -11,7 +11,12 @@ The cross-attention K|V of every attn2 layer (text context + gated audio
 tokens, AudioAttnProcessor :76-122) does not depend on the latent: it is
 computed once per run into persistent buffers and passed to the processors as
 cross_attention_kwargs['context_kv'], so the captured step holds only the
-latent-dependent work.
+latent-dependent work.  The same holds for the time conditioning (sinusoidal
+embedding -> TimestepEmbedding MLP -> all 22 time_emb_proj): it depends on the
+step only, so one run computes it for every step at once (M = steps rows instead
+of four M = 2B launches per step, whose K loops are pure latency) and the step
+selects its row through the device step counter, broadcast to the CFG batch by a
+zero leading stride.
 """
 from __future__ import annotations
 
@@ -40,9 +45,24 @@ class GraphDenoiser:
         self.use_graph = use_graph
         self.graph = None
         self.temb_ch = unet.cfg["block_out_channels"][0]
+        self.temb_table = None   # [steps, 22 x cout] fp16: every resnet's time_emb_proj output per step
+        self.temb_cur = None     # [1, 22 x cout]: this step's row
+
+    def prepare_time(self) -> None:
+        """(Re)compute the time-conditioning table for every step (eager or inside a graph)."""
+        u = self.unet
+        t_sin = torch.cat([ops.timestep_embedding(self.t_table[i:i + 1], None, 1, self.temb_ch)
+                           for i in range(self.steps)])
+        table = u.time_conditioning(t_sin)
+        if self.temb_table is None:
+            self.temb_table = torch.empty_like(table)
+            self.temb_cur = torch.empty((1, table.shape[1]), device=table.device, dtype=table.dtype)
+        self.temb_table.copy_(table)
 
     def prepare_context(self) -> None:
-        """(Re)compute every cross-attention K|V into its persistent buffer (eager)."""
+        """(Re)compute every cross-attention K|V into its persistent buffer, and the
+        time-conditioning table (eager, or captured into the conditioning graph)."""
+        self.prepare_time()
         audio = self.kw.get("audio")
         for attn in self.cross_attns:
             buf = self.context_kv.get(attn)
@@ -50,8 +70,10 @@ class GraphDenoiser:
 
     def _body(self) -> None:
         xin = ops.latent_to_nhwc(self.x, self.unet.in_pad, dup=True)
-        t_sin = ops.timestep_embedding(self.t_table, self.step_idx, 2 * self.b, self.temb_ch)
-        eps = self.unet.forward_nhwc(xin, t_sin, self.ehs, dict(self.kw, context_kv=self.context_kv))
+        torch.index_select(self.temb_table, 0, self.step_idx, out=self.temb_cur)
+        temb_all = self.temb_cur.expand(2 * self.b, self.temb_cur.shape[1])   # zero row stride: one row for all
+        eps = self.unet.forward_nhwc(xin, None, self.ehs, dict(self.kw, context_kv=self.context_kv),
+                                     temb_all=temb_all)
         ops.cfg_ddim_step(eps, self.x, self.g, self.coef, self.step_idx, advance=True)
 
     def capture(self) -> None:

@@ -330,17 +330,26 @@ class UNet2DConditionModel(nn.Module):
                 m.set_processor(processor[f"{n}.processor"] if isinstance(processor, dict) else processor)
 
     # ------------------------------------------------------------ forward
-    def forward_nhwc(self, x: torch.Tensor, t_sin: torch.Tensor, ehs: torch.Tensor,
+    def time_conditioning(self, t_sin: torch.Tensor) -> torch.Tensor:
+        """t_sin [M, 320] fp16 sinusoidal embedding -> every resnet's time_emb_proj(silu(
+        TimestepEmbedding(t))) side by side, [M, 22 x cout] fp16 (resnet r at temb_off)."""
+        temb = self.time_embedding(t_sin)
+        return ops.conv(temb, self.w_temb_all, self.temb_kpad, self.temb_total, ksize=1, bias=self.b_temb_all,
+                        silu_in=True)
+
+    def forward_nhwc(self, x: torch.Tensor, t_sin: torch.Tensor | None, ehs: torch.Tensor,
                      cross_attention_kwargs: dict | None = None,
-                     encoder_attention_mask: torch.Tensor | None = None) -> torch.Tensor:
+                     encoder_attention_mask: torch.Tensor | None = None,
+                     temb_all: torch.Tensor | None = None) -> torch.Tensor:
         """x: [N, H, W, 8] fp16 (latent zero-padded to 8 ch); t_sin: [N, 320] fp16
         sinusoidal embedding; ehs: [N, 77, 768] fp16; encoder_attention_mask: additive
-        key bias [N, 1, 77] for every attn2 (or None). Returns eps [N, H, W, 4] fp16."""
+        key bias [N, 1, 77] for every attn2 (or None); temb_all: precomputed
+        time_conditioning rows [N, 22 x cout] (any row stride, 0 = one row for all) in place
+        of t_sin. Returns eps [N, H, W, 4] fp16."""
         kw = cross_attention_kwargs or {}
         em = encoder_attention_mask
-        temb = self.time_embedding(t_sin)
-        temb_all = ops.conv(temb, self.w_temb_all, self.temb_kpad, self.temb_total, ksize=1, bias=self.b_temb_all,
-                            silu_in=True)
+        if temb_all is None:
+            temb_all = self.time_conditioning(t_sin)
         h = self.conv_in(x)
         skips = [h]
         for blk in self.down_blocks:
