@@ -2,6 +2,7 @@
 // LayerNorm statistics / apply for gfx950.  All HBM-bound: 16-B vector loads,
 // per-block LDS reduction, per-block partials reduced by a second kernel.
 #include "common.h"
+#include <stdlib.h>
 
 namespace c2d {
 
@@ -509,12 +510,21 @@ static int ln_dispatch(const void* x, int m, int c, int ld, float eps, float* st
 
 using namespace c2d;
 
-// rows (pixels) per partial block: about 1024 blocks over the whole launch, at
-// least one full pass of the block's row-threads, at most 128
+// target partial-block count of a launch (C2D_GN_BLOCKS, A/B only).  512: 64^2 x 320 GN
+// 30.5 -> 29.3 us, 32^2 x 640 23.4 -> 20.6 us vs 1024 (graph-replayed, same box; 2048 slower)
+static int gn_target_blocks() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GN_BLOCKS"); v = e ? atoi(e) : 512; if (v < 64) v = 512; }
+    return v;
+}
+
+// rows (pixels) per partial block: about gn_target_blocks() blocks over the whole launch,
+// at least one full pass of the block's row-threads, at most 128
 static int gn_rows_per_block(int n, int c, int hw) {
     const int nch = c >> 3;
     const int r = nch <= 256 ? 256 / nch : 1;
-    long want = ((long)n * hw + 1023) / 1024;
+    const long tb = gn_target_blocks();
+    long want = ((long)n * hw + tb - 1) / tb;
     if (want < r) want = r;
     if (want > 128) want = 128;
     return (int)((want + r - 1) / r * r);
