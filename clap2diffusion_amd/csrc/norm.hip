@@ -520,6 +520,13 @@ static int gn_target_blocks() {
 
 // rows (pixels) per partial block: about gn_target_blocks() blocks over the whole launch,
 // at least one full pass of the block's row-threads, at most 128
+// apply workgroups per launch (C2D_GN_APPLY_BLOCKS, A/B only; default 2048)
+static int gn_apply_blocks() {
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("C2D_GN_APPLY_BLOCKS"); v = e ? atoi(e) : 2048; if (v < 64) v = 2048; }
+    return v;
+}
+
 static int gn_rows_per_block(int n, int c, int hw) {
     const int nch = c >> 3;
     const int r = nch <= 256 ? 256 / nch : 1;
@@ -597,8 +604,8 @@ extern "C" int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, i
     const int nch = (c0 + c1) >> 3;
     if (nch > 512) return C2D_E_SHAPE;
     const int L = nch < 256 ? nch : 256, R = 256 / L;
-    // about 2048 workgroups over the launch, each at least one pass of its rows
-    int bx = (2048 + n - 1) / n;
+    // about gn_apply_blocks() workgroups over the launch, each at least one pass of its rows
+    int bx = (gn_apply_blocks() + n - 1) / n;
     const int maxb = (hw + R - 1) / R;
     if (bx > maxb) bx = maxb;
     if (bx < 1) bx = 1;
