@@ -872,6 +872,14 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
         DmaPlan pl = plan_dma(M, cout, nk, geglu, id, gemm_split());
         if (pl.id) return pl;
     }
+    // narrow outputs (the UNet / VAE conv_out, 4 channels): the 256x128 32x32-MFMA tile, 3
+    // stages (scripts/small_cout.py, forced tiles on one box: UNet conv_out 320 -> 4 at 64^2,
+    // N = 16: 91.3 us on tile 40, 80.5 on the 64x64 tile 3, 49.0 on tile 29; VAE conv_out
+    // 128 -> 4 at 512^2, N = 8: 1332.6 / 874.3 / 725.3 us)
+    if (cout <= 64 && !geglu) {
+        DmaPlan pl = plan_dma(M, cout, nk, geglu, 29, 0);
+        if (pl.id == 29) return pl;
+    }
     // rules from the shape sweeps (scripts/sweep_tiles.sh): the 256x320 interleaved-DMA
     // tile once it (nearly) fills the chip, and with split-K for the long-K convs
     // (9 * cin >= 5760: L1 / L2 resnet and up-block convs); 128x320 below that
