@@ -139,14 +139,19 @@ def cpu_baseline(cores: int | None = None):
     unet_call = float(np.median(tm["unet"]))
     fixed = tm["mel"] + tm["condition"] + tm["vae"]
     s50 = fixed + 50 * unet_call
-    return {"value": round(1.0 / tm["total"], 6), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": f"config c1: 1 x 512^2, 10 DDIM steps, fp32 CPU pipeline (log-mel, HTSAT, projectors, CLIP, "
-                      f"10 CFG-pair UNet calls, VAE) on {cores} threads, 1 run after warm-up",
+    # value in the metric's unit (512^2 images/s at 50 DDIM steps): the measured fixed stages plus
+    # 50 x the measured median CFG-pair UNet call; the measured 10-step c1 rate is its own field
+    return {"value": round(1.0 / s50, 6), "unit": "images/sec (512^2, 50 DDIM steps)", "cores": cores,
+            "kind": "port",
+            "sample": f"config c1 measured (1 x 512^2, 10 DDIM steps, fp32 CPU pipeline: log-mel, HTSAT, projectors, "
+                      f"CLIP, 10 CFG-pair UNet calls, VAE; {cores} threads, 1 run after warm-up), scaled to 50 steps "
+                      f"with the measured per-call UNet time",
             "c1_seconds_per_image": round(tm["total"], 2),
+            "c1_images_per_s_10_steps": round(1.0 / tm["total"], 6),
             "stage_seconds": {"mel": round(tm["mel"], 3), "condition": round(tm["condition"], 3),
                               "unet_call_median": round(unet_call, 3), "unet_total": round(sum(tm["unet"]), 2),
                               "vae": round(tm["vae"], 2)},
-            "images_per_s_50_steps_extrapolated": round(1.0 / s50, 6)}
+            "seconds_per_image_50_steps": round(s50, 2)}
 
 
 def gpu_config_runs(pipe, dev, log):

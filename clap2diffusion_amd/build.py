@@ -20,7 +20,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libc2d_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip", "audio.hip"]
+SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip", "audio.hip", "runtime.hip"]
 # compile units: igemm.hip once per kernel family (C2D_IGEMM_PART, see its header) so
 # the families build in parallel; (source, extra defines, object stem)
 UNITS = [("igemm.hip", (f"C2D_IGEMM_PART={k}",), f"igemm_p{k}") for k in range(4)] + \
@@ -29,8 +29,10 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-at
          "-Wno-unused-result", "-I", str(ROOT / "include")]
 # attention rescales its MFMA accumulators with VALU every tile: keep them in
 # arch VGPRs (gfx950 MFMA can write them) instead of AGPRs + accvgpr copies
-# (-fno-honor-nans: the softmax max chains fold into v_max3 without canonicalising v_max;
-# scores are finite by construction -- masked keys are -1e30, not -inf)
+# (-fno-honor-nans: the softmax max chains fold into v_max3 without canonicalising v_max.
+# Scores are finite unless a caller's attention_mask holds -inf (c2d_attention_fwd_mask):
+# infinities stay honoured, a row with a finite score is exact and an all -inf row comes
+# out NaN as torch's softmax does; tests/test_kernels_gpu.py::test_attention_query_mask)
 EXTRA = {"attention.hip": ["-Xarch_device", "-mllvm=-amdgpu-mfma-vgpr-form=true", "-fno-honor-nans"]}
 
 

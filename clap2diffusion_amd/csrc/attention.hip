@@ -99,7 +99,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                                                        int ldo, int heads, int lq, int lk, float scale_log2,
                                                        int kv_div, int nqb, int abl, int qpb = 1,
                                                        const float* __restrict__ kbias = nullptr, int kb_ldb = 0,
-                                                       int kb_ldh = 0, float kb_mul = 0.f) {
+                                                       int kb_ldh = 0, float kb_mul = 0.f, int kb_ldq = 0) {
     static_assert(!(KBIAS && NEGC), "key bias only on the fma-softmax form");
     using C = AttnCfg<D>;
     constexpr int NT = 64 * NWV;                              // threads; NWV waves x 32 queries per block
@@ -279,17 +279,19 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
 #pragma unroll
                 for (int kg = 0; kg < 4; ++kg) s[qg][kg] += st[qg][kg];
         }
-        if (KBIAS) {   // additive key bias (lane holds keys 16 kg + 4 g + r of its query)
-            const float* kbr = kbias + (size_t)b * kb_ldb + (size_t)h * kb_ldh;
+        if (KBIAS) {   // additive score bias (lane holds keys 16 kg + 4 g + r of query q0 + 16 qg + li)
+            const float* kbb = kbias + (size_t)b * kb_ldb + (size_t)h * kb_ldh;
 #pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
+            for (int qg = 0; qg < 2; ++qg) {
+                const float* kbr = kbb + (size_t)min(q0 + qg * 16 + li, lq - 1) * kb_ldq;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = t * 64 + kg * 16 + g * 4 + r;
-                    const float bb = key < lk ? kbr[key] * kb_mul : 0.f;
-                    s[0][kg][r] += bb;
-                    s[1][kg][r] += bb;
-                }
+                for (int kg = 0; kg < 4; ++kg)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int key = t * 64 + kg * 16 + g * 4 + r;
+                        s[qg][kg][r] += key < lk ? kbr[key] * kb_mul : 0.f;
+                    }
+            }
         }
         if (MASK && (t + 1) * 64 > lk) {  // tail tile: mask keys >= lk
 #pragma unroll
@@ -715,46 +717,22 @@ __global__ void __launch_bounds__(256) attn_pp_kernel(const f16* __restrict__ q,
 // in-flight S tile takes it to 148 VGPR + 24 AGPR = 2 waves/SIMD vs 126 + 40 = 3 for
 // attn_fwd_kernel<40>, and the doubled K/V ring halves the blocks LDS admits, so it is
 // off by default.
-static int attn_abl() {   // C2D_ATTN_ABL=1: timing ablation of the K/V staging (ablation builds only)
-#ifdef C2D_ENABLE_ABLATION
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_ATTN_ABL"); v = e ? atoi(e) : 0; }
-    return v;
-#else
-    return 0;
-#endif
-}
-
-static bool attn_negc() {   // C2D_ATTN_NEGC=0: the fma-per-score softmax (A/B only)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_ATTN_NEGC"); v = e ? atoi(e) : 1; }
-    return v != 0;
-}
-
-static bool attn_res() {   // C2D_ATTN_RES=0: stream K/V tiles for short key sequences too (A/B only)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_ATTN_RES"); v = e ? atoi(e) : 1; }
-    return v != 0;
-}
-
-static bool attn_w8() {   // C2D_ATTN_W8=1: 8-wave blocks for the d = 40 self-attention (A/B)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_ATTN_W8"); v = e ? atoi(e) : 1; }
-    return v != 0;
-}
-
-static int attn_pipelined() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_ATTN_PP"); v = e ? atoi(e) : 0; }
-    return v;
-}
+// A/B switches, read once (runtime.hip tuning()): C2D_ATTN_ABL (ablation builds only:
+// K/V staging skipped), C2D_ATTN_NEGC=0 (fma-per-score softmax), C2D_ATTN_RES=0 (stream
+// K/V tiles for short key sequences too), C2D_ATTN_W8=0 (4-wave d = 40 blocks),
+// C2D_ATTN_PP=1 (the pipelined d = 40 kernel above)
+static int attn_abl() { return tuning().attn_abl; }
+static bool attn_negc() { return tuning().attn_negc != 0; }
+static bool attn_res() { return tuning().attn_res != 0; }
+static bool attn_w8() { return tuning().attn_w8 != 0; }
+static int attn_pipelined() { return tuning().attn_pp; }
 
 // attention with an additive per-key bias: the fma-softmax kernels (resident K/V for
 // lk <= 128, streaming otherwise); the bias is pre-multiplied by 1 / scale
 template <int D>
 static int launch_attn_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                             int batch, int heads, int lq, int lk, float scale, int kv_div, const float* kbias,
-                            int kb_ldb, int kb_ldh, hipStream_t s) {
+                            int kb_ldb, int kb_ldh, int kb_ldq, hipStream_t s) {
     using C = AttnCfg<D>;
     const int nqb = (lq + 127) / 128;
     const int smem = C::K_BYTES + C::V_BYTES;
@@ -767,11 +745,11 @@ static int launch_attn_bias(const void* q, int ldq, const void* k, int ldk, cons
         dim3 g2((unsigned)(ngrp * bhs));
         hipLaunchKernelGGL((attn_fwd_kernel<D, true, false, true, true>), g2, dim3(256), 2 * smem, s, (const f16*)q,
                            ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, sl2, kv_div, nqb,
-                           0, qpb, kbias, kb_ldb, kb_ldh, mul);
+                           0, qpb, kbias, kb_ldb, kb_ldh, mul, kb_ldq);
     } else {
         hipLaunchKernelGGL((attn_fwd_kernel<D, true, false, false, true>), dim3(nqb * batch * heads), dim3(256), smem,
                            s, (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk,
-                           sl2, kv_div, nqb, 0, 1, kbias, kb_ldb, kb_ldh, mul);
+                           sl2, kv_div, nqb, 0, 1, kbias, kb_ldb, kb_ldh, mul, kb_ldq);
     }
     return check_launch();
 }
@@ -905,21 +883,21 @@ extern "C" int c2d_attention_fwd(const void* q, int ldq, const void* k, int ldk,
     }
 }
 
-extern "C" int c2d_attention_fwd_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+extern "C" int c2d_attention_fwd_mask(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
                                       void* o, int ldo, int batch, int heads, int lq, int lk, int d, float scale,
-                                      int kv_div, const float* key_bias, int bias_ld_batch, int bias_ld_head,
-                                      void* stream) {
-    if (!key_bias) return c2d_attention_fwd(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, d, scale, kv_div,
-                                            stream);
+                                      int kv_div, const float* bias, int bias_ld_batch, int bias_ld_head,
+                                      int bias_ld_query, void* stream) {
+    if (!bias) return c2d_attention_fwd(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, d, scale, kv_div,
+                                        stream);
     if (!q || !k || !v || !o || kv_div <= 0) return C2D_E_ARG;
     if (batch <= 0 || heads <= 0 || lq <= 0 || lk <= 0 || scale == 0.f) return C2D_E_SHAPE;
-    if (bias_ld_batch < 0 || bias_ld_head < 0) return C2D_E_SHAPE;
+    if (bias_ld_batch < 0 || bias_ld_head < 0 || bias_ld_query < 0) return C2D_E_SHAPE;
     if ((ldq & 7) || (ldk & 7) || (ldv & 7) || (ldo & 3)) return C2D_E_ALIGN;
     if (!aligned16(q) || !aligned16(k) || !aligned16(v) || ((uintptr_t)o & 7)) return C2D_E_ALIGN;
     if (heads * d > ldq || heads * d > ldk || heads * d > ldv || heads * d > ldo) return C2D_E_SHAPE;
     hipStream_t s = (hipStream_t)stream;
 #define C2D_ATTN_B(DD) launch_attn_bias<DD>(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, scale, kv_div, \
-                                            key_bias, bias_ld_batch, bias_ld_head, s)
+                                            bias, bias_ld_batch, bias_ld_head, bias_ld_query, s)
     switch (d) {
         case 40: return C2D_ATTN_B(40);
         case 64: return C2D_ATTN_B(64);
@@ -928,6 +906,14 @@ extern "C" int c2d_attention_fwd_bias(const void* q, int ldq, const void* k, int
         default: return C2D_E_SHAPE;
     }
 #undef C2D_ATTN_B
+}
+
+extern "C" int c2d_attention_fwd_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                                      void* o, int ldo, int batch, int heads, int lq, int lk, int d, float scale,
+                                      int kv_div, const float* key_bias, int bias_ld_batch, int bias_ld_head,
+                                      void* stream) {
+    return c2d_attention_fwd_mask(q, ldq, k, ldk, v, ldv, o, ldo, batch, heads, lq, lk, d, scale, kv_div, key_bias,
+                                  bias_ld_batch, bias_ld_head, 0, stream);
 }
 
 extern "C" int c2d_window_attention(const void* qkv, int ld_qkv, const int* row_map, int n_windows, int heads, int d,

@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <type_traits>
+#include <mutex>
 #include "../../include/c2d.h"
 
 typedef _Float16 f16;
@@ -43,8 +44,34 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-// thread-local last launch error, exposed as c2d_last_hip_error()
+// thread-local last launch error, exposed as c2d_last_hip_error() (runtime.hip)
 extern thread_local int g_last_hip_error;
+
+// Tuning switches (A/B only; defaults are the measured best), read from the environment
+// once per process under std::call_once (runtime.hip) and immutable afterwards.
+struct Tuning {
+    int gemm_mode, gemm_korder, gemm_lds_epi, gemm_abl;
+    int attn_negc, attn_res, attn_w8, attn_pp, attn_abl;
+    int gn_blocks, gn_apply_blocks, gn_fused_hw;
+};
+const Tuning& tuning();
+// c2d_set_plan_override (tests / sweeps): 0 = the planner decides
+int plan_override_tile();
+int plan_override_split();
+constexpr int kMaxDevices = 64;
+int current_device();
+
+// The per-device kernel table: kernels that declare more than the default 64 KiB of
+// dynamic LDS get hipFuncAttributeMaxDynamicSharedMemorySize once per (kernel, device),
+// under one std::once_flag per device for each kernel instantiation K (thread-safe on a
+// first concurrent call from several host threads, and per device on multi-GPU hosts).
+template <auto K>
+inline void ensure_lds(int bytes) {
+    static std::once_flag once[kMaxDevices];
+    std::call_once(once[current_device()], [bytes] {
+        (void)hipFuncSetAttribute((const void*)K, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    });
+}
 
 inline int check_launch() {
     hipError_t e = hipGetLastError();

@@ -7,8 +7,6 @@
 
 namespace c2d {
 
-thread_local int g_last_hip_error = 0;
-
 __global__ void timestep_emb_kernel(const float* t_table, const int* step_index, int n, int dim, f16* out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int half = dim / 2;
@@ -209,8 +207,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int cout, int c
 
 using namespace c2d;
 
-extern "C" int c2d_last_hip_error(void) { return g_last_hip_error; }
-extern "C" const char* c2d_version(void) { return "c2d_hip gfx950 r1"; }
+extern "C" const char* c2d_version(void) { return "c2d_hip gfx950 r3"; }
 
 extern "C" int c2d_timestep_embedding(const float* t_table, const int* step_index, int n, int dim, void* out,
                                       void* stream) {

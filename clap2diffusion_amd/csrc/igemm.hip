@@ -691,11 +691,7 @@ static void launch_dma(const IgemmParams& p, hipStream_t s) {
     constexpr int smem = ring > epi ? ring : epi;
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     auto k = igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr = true;
-    }
+    ensure_lds<igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
     if (p.ksplit > 1) {
         const size_t total = (size_t)p.M * (p.cout >> 2);
@@ -716,20 +712,12 @@ static void launch(const IgemmParams& p, hipStream_t s) {
 using namespace c2d;
 
 // C2D_GEMM_MODE=2 restricts to the register-staged kernels (A/B comparisons,
-// debugging); default 0 = auto.
-static int gemm_mode() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GEMM_MODE"); v = e ? atoi(e) : 0; }
-    return v;
-}
+// debugging); default 0 = auto.  Read once (runtime.hip tuning()).
+static int gemm_mode() { return tuning().gemm_mode; }
 
-// C2D_GEMM_TILE=k forces DMA tile config k (shape sweeps, the per-tile parity test);
-// 0 = heuristic.  Read per call (not cached) so a test can walk every tile id in one
-// process; the cost is one getenv per launch, outside any captured graph's replay.
-static int gemm_tile() {
-    const char* e = getenv("C2D_GEMM_TILE");
-    return e ? atoi(e) : 0;
-}
+// c2d_set_plan_override(tile, split): force DMA tile config `tile` (shape sweeps, the
+// per-tile parity test); 0 = heuristic.  An explicit setter, never the environment.
+static int gemm_tile() { return plan_override_tile(); }
 
 template <int WM, int WN, int TM, int TN, int ST>
 static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
@@ -813,35 +801,19 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
 
 // C2D_GEMM_ABL: timing ablation of the DMA kernels (1 = no DMA, 2 = no MFMA; m32: 4 = no epilogue,
 // 8 = with 2, no fragment reads either); wrong results by design, so only in -DC2D_ENABLE_ABLATION builds
-static int gemm_abl() {
-#ifdef C2D_ENABLE_ABLATION
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GEMM_ABL"); v = e ? atoi(e) : 0; }
-    return v;
-#else
-    return 0;   // production build: no ablation (common.h C2D_ABL)
-#endif
-}
+static int gemm_abl() { return tuning().gemm_abl; }
 
 // K-step order of the 3x3 DMA kernels.  1 (default): for each 64-channel block all
 // 9 taps, so one block re-reads a (rows + 2 halo image rows) x 64-channel slab from
 // L2 nine times in a row (~1.6 MB live per XCD at 32 resident 256-row blocks).
 // 0: tap-major, the packed weight order, whose reuse distance (rows x cin) spills
 // the 4 MB L2 at cin = 320 and re-fetches the input over the fabric once per tap.
-static int gemm_korder() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GEMM_KORDER"); v = e ? atoi(e) : 1; }
-    return v;
-}
+static int gemm_korder() { return tuning().gemm_korder; }
 
 // C2D_GEMM_LDSEPI=0 lets the 32x32 GEGLU GEMMs store straight from the accumulators:
 // 10 % faster in isolation (L0 320 -> 2 x 1280) but 0.3 % slower in the full step
 // (same-box bench A/B, twice each), so the LDS-staged epilogue stays the default
-static int gemm_lds_epi() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GEMM_LDSEPI"); v = e ? atoi(e) : 1; }
-    return v;
-}
+static int gemm_lds_epi() { return tuning().gemm_lds_epi; }
 
 // the direct 32x32 epilogue stores 4-channel (8-B) runs and loads the bias as float4
 static bool epi_direct_ok(const c2d_conv_desc* d) {
@@ -851,11 +823,8 @@ static bool epi_direct_ok(const c2d_conv_desc* d) {
            (!d->temb || (d->temb_ld % 4) == 0) && (a8 & 7) == 0 && ((uintptr_t)d->bias & 15) == 0;
 }
 
-// C2D_GEMM_SPLIT=s forces s K slices (when the workspace allows); 0 = model
-static int gemm_split() {
-    const char* e = getenv("C2D_GEMM_SPLIT");
-    return e ? atoi(e) : 0;
-}
+// c2d_set_plan_override's split (when the workspace allows); 0 = model
+static int gemm_split() { return plan_override_split(); }
 
 // Tile choice.  Measured on gfx950 over the UNet's conv / linear shapes
 // (scripts/bench_gemm.py, scripts/sweep_tiles.sh): the 256x320 32x32-MFMA tile

@@ -523,11 +523,7 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
     constexpr int smem = m32_smem_bytes<WM, WN, TM, TN, BK, STAGES>();
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE, EACT>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr = true;
-    }
+    ensure_lds<igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE, EACT>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
     if (p.ksplit > 1) {
         const size_t total = (size_t)p.M * (p.cout >> 2);

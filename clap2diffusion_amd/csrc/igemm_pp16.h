@@ -197,11 +197,7 @@ static void launch_pp16(const IgemmParams& p, hipStream_t s) {
     constexpr int smem = ring > epi ? ring : epi;
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     auto k = igemm_pp16_kernel<TN, KS>;
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr = true;
-    }
+    ensure_lds<igemm_pp16_kernel<TN, KS>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(512), smem, s, p);
     if (p.ksplit > 1) {
         const size_t total = (size_t)p.M * (p.cout >> 2);

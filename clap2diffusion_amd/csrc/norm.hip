@@ -512,20 +512,12 @@ using namespace c2d;
 
 // target partial-block count of a launch (C2D_GN_BLOCKS, A/B only).  512: 64^2 x 320 GN
 // 30.5 -> 29.3 us, 32^2 x 640 23.4 -> 20.6 us vs 1024 (graph-replayed, same box; 2048 slower)
-static int gn_target_blocks() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GN_BLOCKS"); v = e ? atoi(e) : 512; if (v < 64) v = 512; }
-    return v;
-}
+static int gn_target_blocks() { return tuning().gn_blocks; }
 
 // rows (pixels) per partial block: about gn_target_blocks() blocks over the whole launch,
 // at least one full pass of the block's row-threads, at most 128
 // apply workgroups per launch (C2D_GN_APPLY_BLOCKS, A/B only; default 2048)
-static int gn_apply_blocks() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GN_APPLY_BLOCKS"); v = e ? atoi(e) : 2048; if (v < 64) v = 2048; }
-    return v;
-}
+static int gn_apply_blocks() { return tuning().gn_apply_blocks; }
 
 static int gn_rows_per_block(int n, int c, int hw) {
     const int nch = c >> 3;
@@ -634,11 +626,7 @@ static int gn_fused_cb(int n, int cin, int groups) {
 // Graph-replayed per call at N = 16 (scripts/bench_norm_graph.py): 8^2 x 1280
 // 16.8 -> 6.2 us, 16^2 x 1280 21.3 -> 13.0 us, but 32^2 x 640 23.1 -> 26.6 us
 // (40-channel chunks read 80-B row pieces over 1024 pixels) and 64^2 2-5x slower.
-static int gn_fused_max_hw() {
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("C2D_GN_FUSED_HW"); v = e ? atoi(e) : 256; }
-    return v;
-}
+static int gn_fused_max_hw() { return tuning().gn_fused_hw; }
 
 static bool gn_use_fused(int n, int cin, int hw, int groups) {
     return gn_fused_cb(n, cin, groups) > 0 && hw <= gn_fused_max_hw();

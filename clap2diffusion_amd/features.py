@@ -70,15 +70,15 @@ class ClapLogMel:
     def crop(self, audios: list) -> list:
         """Host part of preprocess_audio (models/audio_encoder.py:109-129): mono (channel
         mean of a [samples, channels] array) and the first max_len samples of a longer
-        clip; shorter clips are zero-padded by the kernel (lengths < max_len)."""
+        clip; shorter clips are zero-padded by the kernel (lengths < max_len) -- an empty
+        clip included, which becomes max_len samples of silence as the reference's zero-pad
+        (:123-126) makes it (c2d_clap_log_mel: length 0 -> -100 dB)."""
         out = []
         for a in audios:
             a = np.asarray(a, dtype=np.float32)
             if a.ndim > 1:
                 a = a.mean(axis=-1)
             a = a.reshape(-1)
-            if a.size == 0:
-                raise ValueError("empty waveform")
             out.append(a[: self.max_len])
         return out
 
@@ -86,7 +86,10 @@ class ClapLogMel:
         clips = self.crop(audios)
         lengths = np.array([c.size for c in clips], dtype=np.int32)
         offsets = np.concatenate([[0], np.cumsum(lengths[:-1], dtype=np.int64)]).astype(np.int64)
-        wave = torch.from_numpy(np.concatenate(clips)).to(self.device)
+        flat = np.concatenate(clips) if clips else np.zeros(0, np.float32)
+        if flat.size == 0:   # every clip empty: a one-sample buffer nothing reads (all lengths 0)
+            flat = np.zeros(1, np.float32)
+        wave = torch.from_numpy(flat).to(self.device)
         return self.from_device(wave, torch.from_numpy(offsets).to(self.device),
                                 torch.from_numpy(lengths).to(self.device), out)
 

@@ -130,6 +130,34 @@ class record_conv_plans:
         return False
 
 
+class force_plan:
+    """Context manager forcing the implicit-GEMM plan (tile id, K split; 0 = planner) through
+    c2d_set_plan_override -- tests and tuning sweeps only, never the product path."""
+
+    def __init__(self, tile: int, split: int = 0):
+        self.tile, self.split = int(tile), int(split)
+
+    def __enter__(self):
+        from ._lib import check, lib
+        check(lib().c2d_set_plan_override(self.tile, self.split), "c2d_set_plan_override")
+        return self
+
+    def __exit__(self, *exc):
+        from ._lib import lib
+        lib().c2d_set_plan_override(0, 0)
+        return False
+
+
+def plan_override_from_env() -> None:
+    """Opt-in for the tuning scripts: C2D_GEMM_TILE / C2D_GEMM_SPLIT (environment) ->
+    c2d_set_plan_override.  The library itself never reads them."""
+    import os
+    from ._lib import check, lib
+    t, sp = int(os.environ.get("C2D_GEMM_TILE", "0") or 0), int(os.environ.get("C2D_GEMM_SPLIT", "0") or 0)
+    if t or sp:
+        check(lib().c2d_set_plan_override(t, sp), "c2d_set_plan_override")
+
+
 def group_norm_stats(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor,
                      x2: torch.Tensor | None = None):
     """-> (scale, shift) fp32 [N, C] folding GroupNorm(groups, eps) + affine."""
@@ -184,23 +212,28 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, batch: int, hea
               d: int, scale: float | None = None, out: torch.Tensor | None = None,
               key_bias: torch.Tensor | None = None) -> torch.Tensor:
     """q/k/v: 2-D row views [batch*L, >= heads*d] (column slices allowed).
-    key_bias: optional additive per-key score bias, fp32 [batch or 1, heads or 1, lk]
-    (c2d_attention_fwd_bias; size-1 dims broadcast)."""
+    key_bias: optional additive score bias, fp32, either per key [batch|1, heads|1, lk]
+    (c2d_attention_fwd_bias) or per (query, key) [batch|1, heads|1, lq|1, lk]
+    (c2d_attention_fwd_mask); size-1 dims broadcast."""
     _require(q, "q")
     if scale is None:
         scale = 1.0 / math.sqrt(d)
     if out is None:
         out = torch.empty((batch * lq, heads * d), device=q.device, dtype=F16)
-    ldb = ldh = 0
+    ldb = ldh = ldq = 0
     kb = None
     if key_bias is not None:
         kb = key_bias.to(device=q.device, dtype=torch.float32)
-        if kb.dim() != 3 or kb.shape[-1] != lk or kb.shape[0] not in (1, batch) or kb.shape[1] not in (1, heads):
-            raise ValueError(f"key_bias must be [batch|1, heads|1, {lk}], got {tuple(kb.shape)}")
+        if kb.dim() == 3:
+            kb = kb.unsqueeze(2)
+        if (kb.dim() != 4 or kb.shape[-1] != lk or kb.shape[0] not in (1, batch) or kb.shape[1] not in (1, heads)
+                or kb.shape[2] not in (1, lq)):
+            raise ValueError(f"key_bias must be [batch|1, heads|1, ({lq}|1,) {lk}], got {tuple(key_bias.shape)}")
         kb = kb.contiguous()
         ldb = kb.stride(0) if kb.shape[0] > 1 else 0
         ldh = kb.stride(1) if kb.shape[1] > 1 else 0
-    C2D.attention_fwd(q, k, v, batch, heads, lq, lk, d, float(scale), kb, ldb, ldh, out)
+        ldq = kb.stride(2) if kb.shape[2] > 1 else 0
+    C2D.attention_fwd(q, k, v, batch, heads, lq, lk, d, float(scale), kb, ldb, ldh, out, ldq)
     return out
 
 

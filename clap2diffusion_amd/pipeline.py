@@ -13,13 +13,15 @@ Composition contract (SURVEY.md §8(a)): ehs = CLIP([uncond "", prompt]);
 routed tokens repeated for both CFG halves; adapter + Norm-60 and the legacy
 HierarchicalAudioV4 outputs are computed for API fidelity but not fed to the UNet.
 Checkpoints are loaded when present (clap_encoder.pth -> the HTSAT tower,
-audio_projector_stage2.pth 'adapter_state_dict', hierarchical_v4_final.pth; all with
-weights_only=True), otherwise every network uses seeded synthetic weights.
+audio_projector_stage2.pth 'adapter_state_dict', hierarchical_v4_final.pth,
+unet_adapter_final.pth -> the per-level audio processors; all with weights_only=True),
+otherwise every network uses seeded synthetic weights.
 """
 from __future__ import annotations
 
 import argparse
 import os
+import warnings
 import wave
 from pathlib import Path
 
@@ -33,7 +35,7 @@ from .processor import AudioProcessorManager
 from .projectors import AudioAdapter, HierarchicalAudioV4, ImprovedHierarchicalAudioEncoder, normalize_tokens
 from .sampler import GraphDenoiser
 from .scheduler import DDIMScheduler
-from .text_encoder import TextEncoder, tokenize
+from .text_encoder import TextEncoder, make_tokenizer
 from .unet import UNet2DConditionModel
 from .vae import VAEDecoder
 
@@ -112,22 +114,28 @@ class AudioToImageInference:
         self.unet.load_diffusers_state_dict(sd15["unet"] if sd15 else W.synth_unet(self.seed))
         self.manager = AudioProcessorManager(self.unet)
         self.manager.setup_processors(verbose=self.verbose)
-        for level, p in self.manager.level_processors().items():
+        procs = self.manager.level_processors()
+        for level, p in procs.items():
             p.load_state_dict(W.synth_processor_weights(level, self.seed))
+        # the trained processors (audio_proj.*, alpha per level): reference scripts/inference.py:61-65
+        # (also app/gradio_app.py:39-46, scripts/train_stage3.py:78-81); forms: weights.processor_state_dicts
+        unet_adapter_path = self.checkpoint_dir / "unet_adapter_final.pth"
+        if unet_adapter_path.exists():
+            self._log(f"Loading UNet Adapter from {unet_adapter_path}")
+            per_level = W.processor_state_dicts(torch.load(unet_adapter_path, map_location="cpu", weights_only=True),
+                                                self.manager.level_mapping)
+            if not per_level:
+                warnings.warn(f"{unet_adapter_path}: no audio-processor keys (audio_proj.* / alpha) recognised; "
+                              "keeping the current processor weights")
+            for level, sd in per_level.items():
+                if level in procs:
+                    procs[level].load_state_dict(sd)
+        for p in procs.values():
             p.to(dev).eval()
         self.clap = HTSATEncoder().to(dev)
-        clap_path = self.checkpoint_dir / "clap_encoder.pth"   # reference scripts/inference.py:38-41
-        if self.clap_model_path:
-            cp = Path(self.clap_model_path)
-            cp = W.find_weights_file(cp, ("model", "pytorch_model")) if cp.is_dir() else cp
-            self._log(f"Loading CLAP weights from {cp}")
-            self.clap.load_clap_state_dict(W.clap_audio_state_dict(W.load_weights_file(cp)))
-        if clap_path.exists():
-            self._log(f"Loading CLAP encoder from {clap_path}")
-            self.clap.load_clap_state_dict(W.clap_audio_state_dict(
-                torch.load(clap_path, map_location="cpu", weights_only=True)))
-        elif not self.clap_model_path:
-            self.clap.load_clap_state_dict(W.synth_htsat(self.seed))
+        clap_sd, clap_src = W.resolve_clap_weights(self.checkpoint_dir, self.clap_model_path, self.seed)
+        self._log(f"CLAP audio tower: {clap_src}")
+        self.clap.load_clap_state_dict(clap_sd)
         self.hier_encoder = W.fill_module(ImprovedHierarchicalAudioEncoder(), "improved.", self.seed).to(dev).eval()
         adapter_path = self.checkpoint_dir / "audio_projector_stage2.pth"
         self.audio_adapter = W.fill_module(AudioAdapter(), "adapter.", self.seed).to(dev).eval()
@@ -143,6 +151,8 @@ class AudioToImageInference:
             self.hierarchical_model.load_state_dict(torch.load(hpath, map_location=dev, weights_only=True))
         # CLIPTextModel-keyed weights: the SD1.5 text_encoder, else the seeded recipe
         self.text_encoder = TextEncoder(dev, seed=self.seed, state_dict=sd15["text_encoder"] if sd15 else None)
+        # the SD1.5 folder's CLIP BPE tokenizer (tokenizer/vocab.json + merges.txt), else hash ids
+        self.tokenizer = make_tokenizer(self.sd_model_path)
         self.vae = VAEDecoder().to(dev)
         self.vae.load_diffusers_state_dict(sd15["vae"] if sd15 else W.synth_vae_decoder(self.seed))
         self.scheduler = DDIMScheduler()
@@ -172,27 +182,42 @@ class AudioToImageInference:
     def apply_normalization(self, audio_tokens, target_norm=60.0):
         return normalize_tokens(audio_tokens, target_norm)
 
+    def _request_latents(self, n: int, seed) -> torch.Tensor:
+        """Initial latents of n requests as the reference's generate() seeds them
+        (scripts/inference.py:113-116: torch.manual_seed(seed) / np.random.seed(seed) when a seed
+        is given, the RNG left as it is otherwise): each request draws [1, 4, h/8, w/8] from the
+        global CPU generator right after its (re-)seeding, so a given seed always yields
+        initial_latents([seed]) and seed=None draws fresh noise every call."""
+        h, w = self.height // 8, self.width // 8
+        lat = []
+        for _ in range(n):
+            if seed is not None:
+                torch.manual_seed(seed)
+                np.random.seed(seed)
+            lat.append(torch.randn(1, 4, h, w))
+        return torch.cat(lat).to(self.device)
+
     @torch.no_grad()
     def generate(self, audio_path, text_prompt="", num_inference_steps=50, guidance_scale=7.5, seed=None,
                  use_hierarchical=True):
-        if seed is not None:
-            torch.manual_seed(seed)
-            np.random.seed(seed)
         audio = self.load_audio(audio_path)
         img = self.generate_batch(self.mel_features([audio]), [text_prompt], num_inference_steps, guidance_scale,
-                                  seeds=[0 if seed is None else seed], use_hierarchical=use_hierarchical)
+                                  use_hierarchical=use_hierarchical, latents=self._request_latents(1, seed))
         return self.to_pil(img)[0]
 
     def batch_generate(self, audio_paths, text_prompts=None, **kwargs):
+        """The reference runs generate(path, prompt, **kwargs) per item (scripts/inference.py:168-180),
+        so every item is re-seeded with the same seed (the same initial noise for every item) and
+        seed=None leaves the RNG unseeded; here the items run as one batch with those latents."""
         if text_prompts is None:
             text_prompts = [""] * len(audio_paths)
         steps = kwargs.get("num_inference_steps", 50)
         g = kwargs.get("guidance_scale", 7.5)
         seed = kwargs.get("seed", None)
         mel = self.mel_features([self.load_audio(p) for p in audio_paths])
-        seeds = [(0 if seed is None else seed) * 1000 + i for i in range(len(audio_paths))]
-        img = self.generate_batch(mel, list(text_prompts), steps, g, seeds=seeds,
-                                  use_hierarchical=kwargs.get("use_hierarchical", True))
+        img = self.generate_batch(mel, list(text_prompts), steps, g,
+                                  use_hierarchical=kwargs.get("use_hierarchical", True),
+                                  latents=self._request_latents(len(audio_paths), seed))
         return self.to_pil(img)
 
     # ------------------------------------------------------------ batched core
@@ -240,7 +265,7 @@ class AudioToImageInference:
         image size follows the latents ([B, 4, H/8, W/8]; default: the pipeline's size)."""
         b = mel.shape[0]
         if ids is None:
-            ids = (tokenize([""] * b, self.device), tokenize(prompts or [""] * b, self.device))
+            ids = (self.tokenizer([""] * b, self.device), self.tokenizer(prompts or [""] * b, self.device))
         ehs, kw, _ = self.condition(mel, ids[0], ids[1], use_hierarchical)
         if latents is None:
             latents = self.initial_latents(seeds if seeds is not None else list(range(b)))

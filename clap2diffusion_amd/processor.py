@@ -28,39 +28,60 @@ import torch.nn.functional as F
 from . import ops
 
 
-def _as_tokens(x: torch.Tensor) -> torch.Tensor:
-    if x.dim() != 3:
-        raise ValueError("HIP attention processors take [B, L, C] hidden states")
-    return x if x.is_contiguous() else x.contiguous()
+def _as_tokens(x: torch.Tensor):
+    """[B, L, C] token matrix (fp16, contiguous) of the hidden states, and the map back to the
+    caller's form: 4-D [B, C, H, W] input is viewed as [B, H*W, C] and the output transposed
+    back (reference :67-70, :137-138); a non-fp16 input gets its output in its own dtype."""
+    restore = None
+    if x.dim() == 4:
+        b, c, hh, ww = x.shape
+        dt = x.dtype
+        x = x.reshape(b, c, hh * ww).transpose(1, 2)
+
+        def restore(o, b=b, c=c, hh=hh, ww=ww, dt=dt):
+            return o.transpose(-1, -2).reshape(b, c, hh, ww).to(dt)
+    elif x.dim() == 3:
+        if x.dtype != torch.float16:
+            dt = x.dtype
+
+            def restore(o, dt=dt):
+                return o.to(dt)
+    else:
+        raise ValueError(f"attention processors take [B, L, C] or [B, C, H, W] hidden states, got {tuple(x.shape)}")
+    x = x.to(torch.float16)
+    return (x if x.is_contiguous() else x.contiguous()), restore
 
 
-def key_bias_of(attention_mask: Optional[torch.Tensor], batch: int, heads: int, lk: int) -> Optional[torch.Tensor]:
+def key_bias_of(attention_mask: Optional[torch.Tensor], batch: int, heads: int, lk: int,
+                lq: int = 1) -> Optional[torch.Tensor]:
     """attention_mask (additive, as Attention.get_attention_scores adds it to q k^T * scale:
-    reference :129) -> the per-key bias c2d_attention_fwd_bias takes, fp32 [B|1, H|1, lk].
-    Accepted: the key-padding forms -- [lk], [1, lk], [B*H | B | 1, 1, lk] (diffusers'
-    prepare_attention_mask output, or the UNet's encoder_attention_mask bias) and
-    [B | 1, 1, 1, lk].  A mask that varies over queries is rejected: the SD1.5 path never
-    builds one and the flash kernel carries a per-key bias only."""
+    reference :129) -> the score bias c2d_attention_fwd_mask takes, fp32 [B|1, H|1, Lq|1, lk].
+    Accepted: what broadcasts to the [B*H, Lq, Lk] scores the reference's baddbmm forms --
+    [lk], [Lq|1, lk], [B*H | 1, Lq|1, lk] -- plus the per-image forms [B, Lq|1, lk] (the UNet's
+    encoder_attention_mask bias) and 4-D [B|1, H|1, Lq|1, lk]; masks varying over queries
+    included.  Any other shape raises, as the reference's broadcasting would."""
     if attention_mask is None:
         return None
     m = attention_mask
     if m.shape[-1] != lk:
         raise ValueError(f"attention_mask last dim {m.shape[-1]} != number of keys {lk}")
-    if m.dim() == 4 and m.shape[1] == 1 and m.shape[2] == 1:
-        m = m[:, 0]
+    if m.dim() == 4:
+        if m.shape[0] not in (1, batch) or m.shape[1] not in (1, heads) or m.shape[2] not in (1, lq):
+            raise ValueError(f"4-D attention_mask {tuple(m.shape)} does not broadcast to [{batch}, {heads}, {lq}, {lk}]")
+        return m.float()
     if m.dim() == 1:
         m = m.view(1, 1, lk)
     elif m.dim() == 2:
-        if m.shape[0] != 1:
-            raise NotImplementedError("2-D attention_mask must be [1, lk] (per-key)")
-        m = m.view(1, 1, lk)
-    if m.dim() != 3 or m.shape[1] != 1:
-        raise NotImplementedError("attention_mask varying over queries is not supported (per-key masks only)")
-    x = m.shape[0]
+        m = m.view(1, m.shape[0], lk)
+    if m.dim() != 3:
+        raise ValueError(f"attention_mask of shape {tuple(attention_mask.shape)} is not supported")
+    x, q = m.shape[0], m.shape[1]
+    if q not in (1, lq):
+        raise ValueError(f"attention_mask query dim {q} matches neither 1 nor Lq={lq}")
     if x == batch * heads and heads > 1:
-        return m.reshape(batch, heads, lk).float()
+        return m.reshape(batch, heads, q, lk).float()
     if x in (batch, 1):
-        return m.reshape(x, 1, lk).float()
+        return m.reshape(x, 1, q, lk).float()
     raise ValueError(f"attention_mask batch dim {x} matches neither B*heads={batch * heads}, B={batch} nor 1")
 
 
@@ -72,7 +93,7 @@ class AttnProcessor(nn.Module):
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
                  scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
-        x = _as_tokens(hidden_states)
+        x, restore = _as_tokens(hidden_states)
         b, l, c = x.shape
         x2 = x.view(b * l, c)
         heads, d = attn.heads, attn.dim_head
@@ -82,7 +103,7 @@ class AttnProcessor(nn.Module):
             if scale != 1.0:
                 qkv[:, :inner].mul_(scale)
             o = ops.attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], b, heads, l, l, d,
-                              key_bias=key_bias_of(attention_mask, b, heads, l))
+                              key_bias=key_bias_of(attention_mask, b, heads, l, l))
         else:
             cache = cross_attention_kwargs.get("context_kv")
             kv = cache.get(attn) if cache is not None else None
@@ -93,16 +114,13 @@ class AttnProcessor(nn.Module):
             if scale != 1.0:
                 q.mul_(scale)
             o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d,
-                              key_bias=key_bias_of(attention_mask, b, heads, lk))
-        out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
-                             out=None if _residual is None else _residual.reshape(b * l, c))
-        return out.view(b, l, c)
-
+                              key_bias=key_bias_of(attention_mask, b, heads, lk, l))
+        return _project_out(attn, o, b, l, c, _residual, restore)
 
     def context_kv(self, attn, encoder_hidden_states: torch.Tensor, audio: Optional[dict] = None,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """K|V = context @ [W_k; W_v]^T, [B*Lk, 2*inner] fp16 (loop-invariant across denoise steps)."""
-        ehs = _as_tokens(encoder_hidden_states.to(torch.float16))
+        ehs, _ = _as_tokens(encoder_hidden_states.to(torch.float16))
         inner = attn.heads * attn.dim_head
         kv = ops.conv(ehs.reshape(-1, ehs.shape[-1]), attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1, out=out)
         return kv
@@ -162,7 +180,7 @@ class AudioAttnProcessor(nn.Module):
         the latent: the sampler computes it once per request (into `out`, so a
         captured graph keeps reading the same buffer) and hands it back through
         cross_attention_kwargs['context_kv'] on every denoise step."""
-        ehs = _as_tokens(encoder_hidden_states.to(torch.float16))
+        ehs, _ = _as_tokens(encoder_hidden_states.to(torch.float16))
         b = ehs.shape[0]
         inner = attn.heads * attn.dim_head
         audio_tokens = audio[self.level] if (audio is not None and self.level in audio) else None
@@ -190,26 +208,41 @@ class AudioAttnProcessor(nn.Module):
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
                  scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
-        x = _as_tokens(hidden_states)
+        x, restore = _as_tokens(hidden_states)
         b, l, c = x.shape
         heads, d = attn.heads, attn.dim_head
         inner = heads * d
         ehs = encoder_hidden_states
-        if ehs is None:  # self-attention use of the processor (reference :117-118)
-            return AttnProcessor.__call__(self, attn, hidden_states, None, attention_mask, temb, scale, _residual)
-        cache = cross_attention_kwargs.get("context_kv")
-        kv = cache.get(attn) if cache is not None else None
-        if kv is None:
-            kv = self.context_kv(attn, ehs, cross_attention_kwargs.get("audio", None))
-        lk = kv.shape[0] // b
         q = ops.conv(x.view(b * l, c), attn.to_q.weight, attn.kpad_q, inner, ksize=1)
         if scale != 1.0:
             q.mul_(scale)
+        if ehs is None:
+            # reference :115-121: hidden_states = to_q(h) * scale, then encoder_hidden_states =
+            # that projected query, so K / V = to_k / to_v(to_q(h) * scale); no audio injection
+            # (the reference injects only when encoder_hidden_states is given, :86)
+            if attn.to_k.in_features != inner:
+                raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({b * l}x{inner} and "
+                                   f"{attn.to_k.in_features}x{inner}): to_k of this layer does not take the "
+                                   "projected query (reference :120)")
+            kv = ops.conv(q, attn.w_kv, attn.kpad_kv, 2 * inner, ksize=1)
+        else:
+            cache = cross_attention_kwargs.get("context_kv")
+            kv = cache.get(attn) if cache is not None else None
+            if kv is None:
+                kv = self.context_kv(attn, ehs, cross_attention_kwargs.get("audio", None))
+        lk = kv.shape[0] // b
         o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d,
-                          key_bias=key_bias_of(attention_mask, b, heads, lk))
-        out = attn.to_out[0](o, resid=None if _residual is None else _residual.reshape(b * l, c),
-                             out=None if _residual is None else _residual.reshape(b * l, c))
-        return out.view(b, l, c)
+                          key_bias=key_bias_of(attention_mask, b, heads, lk, l))
+        return _project_out(attn, o, b, l, c, _residual, restore)
+
+
+def _project_out(attn, o, b, l, c, residual, restore):
+    """to_out[0] (+ the block residual fused into its epilogue when the UNet passes it),
+    back in the caller's layout / dtype."""
+    out = attn.to_out[0](o, resid=None if residual is None else residual.reshape(b * l, c),
+                         out=None if residual is None else residual.reshape(b * l, c))
+    out = out.view(b, l, c)
+    return out if restore is None else restore(out)
 
 
 class AudioProcessorManager:

@@ -5,9 +5,10 @@ with the quick_gelu epilogue -> fc2 GEMM + residual; final LN.  Semantics of
 transformers CLIPTextModel (modeling_clip.py CLIPTextTransformer), which the SD1.5
 pipeline the reference drives loads (scripts/inference.py:30-33).
 
-No tokenizer vocabulary or weights exist offline, so prompts map to fixed,
-deterministic token-id lists (BOS, per-word ids from a stable hash, EOS, EOS
-padding to 77 as in SD1.5) and the tower loads a CLIPTextModel-keyed state dict,
+Prompts become token ids through the SD1.5 folder's CLIP BPE tokenizer (tokenizer/vocab.json +
+merges.txt; clap2diffusion_amd/tokenizer.py) when one is given (make_tokenizer); with no
+vocabulary offline they map to fixed, deterministic token-id lists instead (BOS, per-word ids
+from a stable hash, EOS, EOS padding to 77 as in SD1.5).  The tower loads a CLIPTextModel-keyed state dict,
 by default the seeded recipe weights.synth_clip_text (the SD1.5 architecture:
 12 layers, width 768, 12 heads, quick_gelu).  The product never imports
 transformers; the tests load the same state dict into transformers'
@@ -34,7 +35,21 @@ def prompt_to_ids(prompt: str) -> list[int]:
 
 
 def tokenize(prompts: list[str], device=None) -> torch.Tensor:
+    """The offline fallback: hash ids (prompt_to_ids), [B, 77]."""
     return torch.tensor([prompt_to_ids(p) for p in prompts], dtype=torch.long, device=device)
+
+
+def make_tokenizer(sd_model_path=None):
+    """prompts, device -> [B, 77] token ids: the CLIP BPE tokenizer of an SD1.5 diffusers
+    folder (its tokenizer/ subfolder, or the folder itself) when it holds vocab.json and
+    merges.txt, else the hash-id fallback `tokenize`."""
+    if sd_model_path is not None:
+        from pathlib import Path
+        from .tokenizer import CLIPBPETokenizer
+        for d in (Path(sd_model_path) / "tokenizer", Path(sd_model_path)):
+            if (d / "vocab.json").exists() and (d / "merges.txt").exists():
+                return CLIPBPETokenizer.from_folder(d)
+    return tokenize
 
 
 class TextEncoder:

@@ -141,14 +141,18 @@ def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, out: Tensor) -
 
 @custom_op("c2d::attention_fwd", mutates_args=("out",), device_types=_CU)
 def attention_fwd(q: Tensor, k: Tensor, v: Tensor, batch: int, heads: int, lq: int, lk: int, d: int, scale: float,
-                  key_bias: Optional[Tensor], bias_ld_batch: int, bias_ld_head: int, out: Tensor) -> None:
+                  key_bias: Optional[Tensor], bias_ld_batch: int, bias_ld_head: int, out: Tensor,
+                  bias_ld_query: int = 0) -> None:
+    """c2d_attention_fwd, or c2d_attention_fwd_mask with an additive score bias (bias_ld_query 0:
+    a per-key bias, else a query-varying one)."""
     if key_bias is None:
         check(lib().c2d_attention_fwd(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
                                       out.stride(0), batch, heads, lq, lk, d, scale, 1, stream_ptr()), "c2d_attention_fwd")
     else:
-        check(lib().c2d_attention_fwd_bias(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
+        check(lib().c2d_attention_fwd_mask(ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0), ptr(out),
                                            out.stride(0), batch, heads, lq, lk, d, scale, 1, ptr(key_bias),
-                                           bias_ld_batch, bias_ld_head, stream_ptr()), "c2d_attention_fwd_bias")
+                                           bias_ld_batch, bias_ld_head, bias_ld_query, stream_ptr()),
+              "c2d_attention_fwd_mask")
 
 
 @custom_op("c2d::attention_small", mutates_args=("out",), device_types=_CU)

@@ -319,6 +319,77 @@ def clap_audio_state_dict(ck: dict) -> "OrderedDict[str, torch.Tensor]":
     return out
 
 
+PROCESSOR_KEYS = ("audio_proj.0.weight", "audio_proj.0.bias", "audio_proj.3.weight", "audio_proj.3.bias", "alpha")
+
+
+def processor_state_dicts(ck: dict, level_mapping: dict) -> "dict[str, OrderedDict]":
+    """Per-level AudioAttnProcessor state dicts (audio_proj.0/3 weight+bias, alpha) from a
+    unet_adapter_final.pth (reference scripts/inference.py:61-65, app/gradio_app.py:39-46,
+    scripts/train_stage3.py:78-81; the reference never writes the file, so every natural form
+    is read):
+      {"early"|"mid"|"late": {audio_proj..., alpha}}            per-level dicts
+      {"<level>.audio_proj.0.weight", ...}                       flat, level-prefixed (any prefix
+                                                                 ending in the level name)
+      {"<processor name>.audio_proj.0.weight", ...}              keyed by unet.attn_processors
+                                                                 names (diffusers AttnProcsLayers),
+                                                                 e.g. down_blocks.0....attn2.processor.*
+      {"audio_proj.0.weight", ...}                               one processor for every level
+    optionally wrapped in {"state_dict" | "model_state_dict" | "processor_state_dict" |
+    "unet_adapter_state_dict" | "processors": ...}.  level_mapping: AudioProcessorManager's
+    {level: [processor names]}.  Returns {} when nothing is recognised."""
+    for wrap in ("state_dict", "model_state_dict", "processor_state_dict", "unet_adapter_state_dict", "processors"):
+        if isinstance(ck.get(wrap), dict):
+            ck = ck[wrap]
+    out: "dict[str, OrderedDict]" = {}
+    if all(isinstance(ck.get(lv), dict) for lv in ("early", "mid", "late") if lv in ck) and \
+            any(isinstance(ck.get(lv), dict) for lv in ("early", "mid", "late")):
+        for lv in ("early", "mid", "late"):
+            if isinstance(ck.get(lv), dict) and all(k in ck[lv] for k in PROCESSOR_KEYS):
+                out[lv] = OrderedDict((k, ck[lv][k]) for k in PROCESSOR_KEYS)
+        return out
+    if all(k in ck for k in PROCESSOR_KEYS):
+        return {lv: OrderedDict((k, ck[k]) for k in PROCESSOR_KEYS) for lv in ("early", "mid", "late")}
+    name_level = {n.rsplit(".processor", 1)[0]: lv for lv, names in level_mapping.items() for n in names}
+    for k, v in ck.items():
+        for pk in PROCESSOR_KEYS:
+            if not k.endswith("." + pk):
+                continue
+            prefix = k[: -len(pk) - 1]
+            stem = prefix[: -len(".processor")] if prefix.endswith(".processor") else prefix
+            lv = name_level.get(stem)
+            if lv is None:
+                last = prefix.rsplit(".", 1)[-1]
+                lv = last if last in ("early", "mid", "late") else None
+            if lv is not None:
+                out.setdefault(lv, OrderedDict())[pk] = v
+    return {lv: OrderedDict((k, sd[k]) for k in PROCESSOR_KEYS) for lv, sd in out.items()
+            if all(k in sd for k in PROCESSOR_KEYS)}
+
+
+def resolve_clap_weights(checkpoint_dir, clap_model_path=None, seed: int = 0):
+    """(state dict, source) for the HTSAT tower, in the pipeline's order of precedence:
+      1. an explicit clap_model_path (--clap_model: a ClapModel weights file or folder) -- what
+         the user asked for wins;
+      2. checkpoint_dir/clap_encoder.pth (reference scripts/inference.py:38-41, which only
+         announces the file: it never loads or writes it, so its format is open) when it holds
+         CLAP audio-tower keys in a clap_audio_state_dict form; a file without them is reported
+         (warnings.warn) and skipped, as the reference carries on;
+      3. the seeded synthetic recipe synth_htsat(seed)."""
+    import warnings
+    from pathlib import Path
+    if clap_model_path:
+        cp = Path(clap_model_path)
+        cp = find_weights_file(cp, ("model", "pytorch_model")) if cp.is_dir() else cp
+        return clap_audio_state_dict(load_weights_file(cp)), f"--clap_model {cp}"
+    path = Path(checkpoint_dir) / "clap_encoder.pth"
+    if path.exists():
+        try:
+            return clap_audio_state_dict(torch.load(path, map_location="cpu", weights_only=True)), str(path)
+        except KeyError as e:
+            warnings.warn(f"{path}: {e}; keeping the seeded CLAP weights")
+    return synth_htsat(seed), f"seeded synthetic weights (seed {seed})"
+
+
 # ------------------------------------------------------------------ checkpoint files
 def load_weights_file(path) -> dict:
     """A state dict from a .safetensors file (safetensors loader) or a torch .bin / .pt /

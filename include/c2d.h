@@ -110,10 +110,19 @@ size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d);
  * access): tile_id = the LDS-DMA tile configuration (0 = the register-staged kernel of
  * descriptors with a prologue / upsampled view), ksplit = K slices (1 = no split-K;
  * reflects d->ws / d->ws_bytes as the launch would).  Lets callers and the per-tile
- * parity test (tests/test_kernels_gpu.py) see which kernel ran; C2D_GEMM_TILE /
- * C2D_GEMM_SPLIT in the environment override the planner (tuning and tests only).
+ * parity test (tests/test_kernels_gpu.py) see which kernel ran; c2d_set_plan_override
+ * forces a plan (tuning and tests only).
  */
 int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit);
+
+/*
+ * Test / tuning hook: force the LDS-DMA tile configuration (tile_id, one of the ids
+ * c2d_conv2d_igemm_plan reports) and the K split (ksplit; 0 = the planner's) of every
+ * later eligible c2d_conv2d_igemm call in the process; c2d_set_plan_override(0, 0)
+ * restores the planner.  Process-wide (atomic), set explicitly: the library never reads
+ * a plan from the environment.  C2D_E_ARG for negative values or ksplit > 64.
+ */
+int c2d_set_plan_override(int tile_id, int ksplit);
 
 /*
  * GroupNorm statistics folded with the affine into per-(image, channel) scale /
@@ -192,12 +201,29 @@ int c2d_attention_fwd(const void* q, int ldq, const void* k, int ldk, const void
  * key-padding form diffusers builds from encoder_attention_mask, (1 - keep) * -10000):
  *   S[b, h, i, j] = Q.K * scale + key_bias[b * bias_ld_batch + h * bias_ld_head + j]
  * fp32 bias, natural-log units; strides 0 broadcast over images / heads.  key_bias NULL
- * is exactly c2d_attention_fwd.  Per-query masks are not representable here.
+ * is exactly c2d_attention_fwd.  Bias entries may be -inf (SDPA-style boolean masks) or
+ * finfo(float).min: a row with at least one finite score is exact; a row whose every
+ * score is -inf comes out NaN, as torch's softmax of such a row does (the reference
+ * path, get_attention_scores + softmax); a row of finfo.min entries comes out as the
+ * uniform average of V, as torch's does.
  */
 int c2d_attention_fwd_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
                            void* o, int ldo, int batch, int heads, int lq, int lk, int d, float scale,
                            int kv_div, const float* key_bias, int bias_ld_batch, int bias_ld_head,
                            void* stream);
+
+/*
+ * The general form: any attention_mask broadcastable to [batch*heads, lq, lk], as the
+ * reference processor hands it unchanged to get_attention_scores
+ * (models/audio_attention_processor.py:129; diffusers baddbmm(mask, q, k^T, beta=1,
+ * alpha=scale)), including masks that vary over queries:
+ *   S[b, h, i, j] = Q.K * scale + bias[b * bias_ld_batch + h * bias_ld_head + i * bias_ld_query + j]
+ * Strides 0 broadcast.  bias_ld_query = 0 is c2d_attention_fwd_bias; same -inf rules.
+ */
+int c2d_attention_fwd_mask(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                           void* o, int ldo, int batch, int heads, int lq, int lk, int d, float scale,
+                           int kv_div, const float* bias, int bias_ld_batch, int bias_ld_head,
+                           int bias_ld_query, void* stream);
 
 /*
  * Swin window attention of the HTSAT tower: tokens gathered through row_map

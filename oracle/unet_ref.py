@@ -50,6 +50,48 @@ def timestep_embedding(t: torch.Tensor, dim: int = 320) -> torch.Tensor:
     return torch.cat([emb[:, half:], emb[:, :half]], dim=-1)  # flip_sin_to_cos
 
 
+def processor_call(w: dict, proc_w: dict | None, h: torch.Tensor, ehs: torch.Tensor | None, audio: dict | None,
+                   level: str, heads: int = 8, mask: torch.Tensor | None = None, scale: float = 1.0,
+                   mode: str = "add") -> torch.Tensor:
+    """The reference AudioAttnProcessor.__call__ (models/audio_attention_processor.py:62-145) on
+    an Attention with weights w (to_q / to_k / to_v / to_out.0), fp32:
+      :67-70   4-D [B, C, H, W] input viewed as [B, H*W, C]
+      :86-109  audio injection only when encoder_hidden_states is given (Add-FiLM or concat)
+      :115-121 q = to_q(h) * scale; with no encoder_hidden_states, K / V come from that
+               projected query (encoder_hidden_states = hidden_states after :115)
+      :129     get_attention_scores: baddbmm(mask, q, k^T, beta=1, alpha=d^-0.5), softmax
+      :137-138 output transposed back to [B, C, H, W]."""
+    nd4 = h.dim() == 4
+    if nd4:
+        b, c, hh, ww = h.shape
+        h = h.reshape(b, c, hh * ww).transpose(1, 2)
+    if ehs is not None and audio is not None and level in audio and proc_w is not None:
+        a = F.linear(audio[level].float(), proc_w["audio_proj.0.weight"], proc_w["audio_proj.0.bias"])
+        a = F.linear(F.gelu(a), proc_w["audio_proj.3.weight"], proc_w["audio_proj.3.bias"])
+        if mode == "add":
+            ehs = ehs + torch.sigmoid(proc_w["alpha"].float()) * a.mean(dim=1, keepdim=True)
+        else:
+            if a.shape[1] > 4:
+                a = F.adaptive_avg_pool1d(a.transpose(1, 2), 4).transpose(1, 2)
+            ehs = torch.cat([ehs, a], dim=1)
+    q = F.linear(h, w["to_q.weight"]) * scale
+    ctx = q if ehs is None else ehs
+    k, v = F.linear(ctx, w["to_k.weight"]), F.linear(ctx, w["to_v.weight"])
+    b, lq, inner = q.shape
+    d = inner // heads
+
+    def hb(t):
+        return t.reshape(b, t.shape[1], heads, d).permute(0, 2, 1, 3).reshape(b * heads, t.shape[1], d)
+    s = torch.bmm(hb(q), hb(k).transpose(1, 2)) * d ** -0.5
+    if mask is not None:
+        s = s + mask
+    o = torch.bmm(s.softmax(-1), hb(v)).reshape(b, heads, lq, d).permute(0, 2, 1, 3).reshape(b, lq, inner)
+    o = F.linear(o, w["to_out.0.weight"], w.get("to_out.0.bias"))
+    if nd4:
+        o = o.transpose(-1, -2).reshape(b, c, hh, ww)
+    return o
+
+
 class UNetRef:
     def __init__(self, sd: dict, processors: dict | None = None, heads: int = 8, groups: int = 32):
         self.sd = {k: v.float() for k, v in sd.items()}

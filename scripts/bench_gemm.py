@@ -9,6 +9,8 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from clap2diffusion_amd import ops  # noqa: E402
 
+ops.plan_override_from_env()   # C2D_GEMM_TILE / C2D_GEMM_SPLIT (tuning runs only)
+
 dev = torch.device("cuda")
 N = 16
 SHAPES = [  # (name, ksize, h, cin, cout, M-rows for linear)

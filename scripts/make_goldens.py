@@ -12,6 +12,11 @@ Run here (not on the GPU box, where /root/reference does not exist):
                   the module only uses for type names at :10) driving a minimal restatement of the
                   diffusers Attention helpers it calls, at the four SD1.5 (C, heads*d) shapes, in
                   "add" and "concat" modes.
+  processor_ext.npz  the same processor on the paths the SD1.5 pipeline does not take: the
+                  self-attention branch (encoder_hidden_states=None: K / V from the projected
+                  query, :115-121), 4-D [B, C, H, W] hidden states (:67-70, :137-138) and
+                  attention masks passed to get_attention_scores (:129), including one that
+                  varies over queries.
   htsat.npz       transformers ClapModel.get_audio_features (the call at
                   models/audio_encoder.py:171-174) on synthetic HTSAT weights and seeded mel input.
 Only inputs and outputs are stored; weights are regenerated from their seeds.
@@ -87,6 +92,8 @@ class MiniAttention(nn.Module):
     def get_attention_scores(self, q, k, mask=None):
         s = torch.baddbmm(torch.empty(q.shape[0], q.shape[1], k.shape[1]), q, k.transpose(-1, -2), beta=0,
                           alpha=self.scale)
+        if mask is not None:   # diffusers 0.23.1: baddbmm(mask, q, k^T, beta=1, alpha=scale)
+            s = torch.baddbmm(mask, q, k.transpose(-1, -2), beta=1, alpha=self.scale)
         return s.softmax(dim=-1)
 
 
@@ -137,6 +144,46 @@ def main():
                 out = proc(attn, h, encoder_hidden_states=ehs, audio={"mid": audio})
             cases[f"c{c}_l{lq}_{mode}_out"] = out.numpy()
     np.savez_compressed(OUT / "processor.npz", **cases)
+
+    # ---------------- processor: self-attention branch, 4-D input, attention masks
+    ext = {}
+    for c, lq, seed in ((320, 48, 200), (640, 32, 201)):   # self-attention layers (to_k / to_v take C)
+        gg = torch.Generator().manual_seed(seed)
+        attn = MiniAttention(c, c, 8, gg).eval()
+        h = torch.randn(2, lq, c, generator=gg)
+        proc = AudioAttnProcessor(level="early", audio_dim=768, hidden_dim=768, mode="add").eval()
+        proc.load_state_dict(synth_processor_weights("early", seed=seed))
+        with torch.no_grad():
+            out = proc(attn, h, encoder_hidden_states=None, audio={"early": audio})
+        ext[f"self_c{c}_l{lq}_h"], ext[f"self_c{c}_l{lq}_out"] = h.numpy(), out.numpy()
+    for c, hh, ww, seed in ((320, 6, 8, 210), (640, 4, 4, 211)):   # 4-D [B, C, H, W] cross-attention input
+        gg = torch.Generator().manual_seed(seed)
+        attn = MiniAttention(c, 768, 8, gg).eval()
+        h4 = torch.randn(2, c, hh, ww, generator=gg)
+        proc = AudioAttnProcessor(level="mid", audio_dim=768, hidden_dim=768, mode="add").eval()
+        proc.load_state_dict(synth_processor_weights("mid", seed=seed))
+        with torch.no_grad():
+            out = proc(attn, h4, encoder_hidden_states=ehs, audio={"mid": audio})
+        ext[f"nd4_c{c}_{hh}x{ww}_h"], ext[f"nd4_c{c}_{hh}x{ww}_out"] = h4.numpy(), out.numpy()
+    for c, lq, form, seed in ((640, 32, "query", 220), (320, 48, "key", 221)):   # attention_mask forms
+        gg = torch.Generator().manual_seed(seed)
+        attn = MiniAttention(c, 768, 8, gg).eval()
+        h = torch.randn(2, lq, c, generator=gg)
+        if form == "query":   # [B*H, Lq, Lk], varies over queries
+            mask = torch.randn(2 * 8, lq, 77, generator=gg) * 2.0
+            mask = mask.masked_fill(torch.rand(2 * 8, lq, 77, generator=gg) < 0.3, -10000.0)
+        else:                 # [B*H, 1, Lk] key padding (prepare_attention_mask's form)
+            keep = torch.ones(2, 77)
+            keep[0, 20:] = 0
+            keep[1, 60:] = 0
+            mask = ((1.0 - keep) * -10000.0).repeat_interleave(8, dim=0).unsqueeze(1)
+        proc = AudioAttnProcessor(level="late", audio_dim=768, hidden_dim=768, mode="add").eval()
+        proc.load_state_dict(synth_processor_weights("late", seed=seed))
+        with torch.no_grad():
+            out = proc(attn, h, encoder_hidden_states=ehs, attention_mask=mask, audio={"late": audio})
+        ext[f"mask_{form}_c{c}_l{lq}_h"], ext[f"mask_{form}_c{c}_l{lq}_mask"] = h.numpy(), mask.numpy()
+        ext[f"mask_{form}_c{c}_l{lq}_out"] = out.numpy()
+    np.savez_compressed(OUT / "processor_ext.npz", **ext)
 
     # ---------------- HTSAT (transformers ClapModel, the reference's CLAP dependency)
     from transformers import ClapConfig, ClapModel

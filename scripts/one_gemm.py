@@ -8,6 +8,8 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from clap2diffusion_amd import ops  # noqa: E402
 
+ops.plan_override_from_env()   # C2D_GEMM_TILE / C2D_GEMM_SPLIT (tuning runs only)
+
 k, h, cin, cout = (int(a) for a in sys.argv[1:5])
 iters = int(sys.argv[5]) if len(sys.argv) > 5 else 10
 N = 16

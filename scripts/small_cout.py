@@ -21,9 +21,9 @@ for name, n, h, cin, cout in [("unet conv_out", 16, 64, 320, 4), ("vae conv_out"
     ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w, b, padding=1).permute(0, 2, 3, 1)
     for t in (0, 40, 7, 1, 2, 3, 29):
         if t:
-            os.environ["C2D_GEMM_TILE"] = str(t)
+            ops.force_plan(t, 0).__enter__()
         else:
-            os.environ.pop("C2D_GEMM_TILE", None)
+            ops.force_plan(0, 0).__enter__()
         with ops.record_conv_plans() as pl:
             ops.conv(x, wp, kp, cout, ksize=3, bias=b, out=out)
         for _ in range(2):
@@ -37,4 +37,4 @@ for name, n, h, cin, cout in [("unet conv_out", 16, 64, 320, 4), ("vae conv_out"
         err = ((out.float() - ref).norm() / ref.norm()).item()
         print(f"{name:16s} forced {t:2d} plan {pl[0]} {e0.elapsed_time(e1) / 10 * 1e3:8.1f} us  relerr {err:.1e}",
               flush=True)
-    os.environ.pop("C2D_GEMM_TILE", None)
+    ops.force_plan(0, 0).__enter__()

@@ -1,5 +1,5 @@
 """(tile, split-K) sweep of the under-filled UNet conv / GEMM shapes (N = 16), one process:
-C2D_GEMM_TILE / C2D_GEMM_SPLIT are read per call.  Prints the default plan's time and the
+The plan is forced through c2d_set_plan_override (ops.force_plan).  Prints the default plan's time and the
 best forced (tile, split) per shape.  python scripts/sweep_split.py"""
 import math
 import os
@@ -47,8 +47,7 @@ for name, k, h, cin, cout, res in SHAPES:
     wp, kp = ops.pack_conv_weight(w)
     out = torch.empty(N, h, h, cout, device=dev, dtype=torch.float16)
     fn = lambda: ops.conv(x, wp, kp, cout, ksize=k, bias=b, resid=r, out=out)  # noqa: E731
-    os.environ.pop("C2D_GEMM_TILE", None)
-    os.environ.pop("C2D_GEMM_SPLIT", None)
+    ops.force_plan(0, 0).__enter__()
     with ops.record_conv_plans() as pl:
         fn()
     base = timeit(fn)
@@ -56,8 +55,7 @@ for name, k, h, cin, cout, res in SHAPES:
     res_t = []
     for t in TILES:
         for s in SPLITS:
-            os.environ["C2D_GEMM_TILE"] = str(t)
-            os.environ["C2D_GEMM_SPLIT"] = str(s)
+            ops.force_plan(t, s).__enter__()
             with ops.record_conv_plans() as pl2:
                 fn()
             if pl2[0] != (t, s):
@@ -65,8 +63,7 @@ for name, k, h, cin, cout, res in SHAPES:
             us = timeit(fn)
             err = ((out.float() - ref).norm() / ref.norm()).item()
             res_t.append((us, t, s, err))
-    os.environ.pop("C2D_GEMM_TILE", None)
-    os.environ.pop("C2D_GEMM_SPLIT", None)
+    ops.force_plan(0, 0).__enter__()
     res_t.sort()
     best = " ".join(f"({t},{s}) {us:.1f}" for us, t, s, _ in res_t[:5])
     print(f"{name:26s} default {pl[0]} {base:7.1f} us | best: {best} | max relerr {max(e for *_, e in res_t):.1e}",

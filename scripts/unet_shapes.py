@@ -13,6 +13,8 @@ import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from clap2diffusion_amd import ops  # noqa: E402
+
+ops.plan_override_from_env()   # C2D_GEMM_TILE / C2D_GEMM_SPLIT (tuning runs only)
 from clap2diffusion_amd.processor import AudioProcessorManager  # noqa: E402
 from clap2diffusion_amd.unet import UNet2DConditionModel  # noqa: E402
 from clap2diffusion_amd.weights import synth_unet  # noqa: E402

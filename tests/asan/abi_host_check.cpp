@@ -125,6 +125,24 @@ int main() {
     CHECK(c2d_attention_fwd(buf + 2, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_ALIGN);
     CHECK(c2d_attention_fwd(buf, 40, buf, 40, buf, 40, buf, 40, 0, 1, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_SHAPE);
     CHECK(c2d_attention_fwd(buf, 40, buf, 40, buf, 40, buf, 40, 1, 2, 8, 8, 40, 0.1f, 1, nullptr) == C2D_E_SHAPE);
+    // the general-mask entry: validation before launch, negative strides rejected
+    CHECK(c2d_attention_fwd_mask(nullptr, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.1f, 1,
+                                 (const float*)buf, 0, 0, 8, nullptr) == C2D_E_ARG);
+    CHECK(c2d_attention_fwd_mask(buf, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.1f, 1,
+                                 (const float*)buf, 0, 0, -8, nullptr) == C2D_E_SHAPE);
+    CHECK(c2d_attention_fwd_mask(buf, 40, buf, 40, buf, 40, buf, 40, 1, 1, 8, 8, 40, 0.0f, 1,
+                                 (const float*)buf, 0, 0, 8, nullptr) == C2D_E_SHAPE);
+    // the explicit plan override (tests / sweeps): forced tile and split reach the planner, 0 restores it
+    {
+        c2d_conv_desc f = desc(4, 16, 16, 320, 0, 3, 1, 640, C2D_ACT_NONE);
+        int t0, s0, t1, s1;
+        CHECK(c2d_conv2d_igemm_plan(&f, &t0, &s0) == C2D_OK);
+        CHECK(c2d_set_plan_override(7, 0) == C2D_OK);
+        CHECK(c2d_conv2d_igemm_plan(&f, &t1, &s1) == C2D_OK && t1 == 7);
+        CHECK(c2d_set_plan_override(-1, 0) == C2D_E_ARG && c2d_set_plan_override(1, 65) == C2D_E_ARG);
+        CHECK(c2d_set_plan_override(0, 0) == C2D_OK);
+        CHECK(c2d_conv2d_igemm_plan(&f, &t1, &s1) == C2D_OK && t1 == t0 && s1 == s0);
+    }
     CHECK(c2d_groupnorm_workspace_size(16, 320, 4096) > 0);
     CHECK(c2d_version() != nullptr && std::strlen(c2d_version()) > 0);
 

@@ -10,6 +10,11 @@ if str(ROOT) not in sys.path:
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 
+def pytest_sessionfinish(session, exitstatus):
+    from tests import parity_log
+    parity_log.write(os.environ.get("C2D_PARITY_LOG", str(ROOT / "gpurun_out" / "parity_metrics.tsv")))
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and the built libc2d_hip.so")
     config.addinivalue_line("markers", "slow: long-running CPU test")

@@ -1,4 +1,4 @@
-"""AddressSanitizer run of the library's host code (SURVEY.md §5 sanitizers row): the five
+"""AddressSanitizer run of the library's host code (SURVEY.md §5 sanitizers row): the
 HIP sources compiled with -fsanitize=address on the host side (-Xarch_host; nothing is
 launched) and linked into tests/asan/abi_host_check.cpp, which sweeps the GEMM planner /
 workspace queries over the model shapes and a random sweep and drives every validation path
@@ -11,9 +11,11 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-# igemm.hip in its four kernel-family parts, as the library build compiles it
-UNITS = [("igemm.hip", f"-DC2D_IGEMM_PART={k}", f"igemm_p{k}") for k in range(4)] + \
-        [(s, None, Path(s).stem) for s in ["norm.hip", "attention.hip", "elementwise.hip", "audio.hip"]]
+# the library's compile units as clap2diffusion_amd/build.py compiles them (igemm.hip in its
+# four kernel-family parts, runtime.hip with the tuning / plan-override / per-device state)
+from clap2diffusion_amd.build import UNITS as _BUILD_UNITS  # noqa: E402
+
+UNITS = [(src, " ".join(f"-D{d}" for d in defs) or None, stem) for src, defs, stem in _BUILD_UNITS]
 # ASAN on the host side only (-Xarch_host before each -fsanitize=); device code builds as usual
 FLAGS = ["--offload-arch=gfx950", "-O1", "-g", "-Xarch_host", "-fsanitize=address", "-Xarch_host",
          "-fno-omit-frame-pointer", "-std=c++17", "-I", str(ROOT / "include"),

@@ -22,11 +22,11 @@ def fill(module, tag):
     return module.eval()
 
 
-def mini_attention_weights(c, seed):
-    """Same draw order as scripts/make_goldens.py:MiniAttention."""
+def mini_attention_weights(c, seed, ctx=768):
+    """Same draw order as scripts/make_goldens.py:MiniAttention (ctx = c: a self-attention layer)."""
     g = torch.Generator().manual_seed(seed)
     w = {}
-    for name, (o, i, bias) in (("to_q", (c, c, False)), ("to_k", (c, 768, False)), ("to_v", (c, 768, False)),
+    for name, (o, i, bias) in (("to_q", (c, c, False)), ("to_k", (c, ctx, False)), ("to_v", (c, ctx, False)),
                                ("to_out.0", (c, c, True))):
         w[name + ".weight"] = torch.randn((o, i), generator=g) / i ** 0.5
         if bias:
@@ -99,6 +99,28 @@ def test_oracle_processor_matches_reference(c, l, mode):
         ctx = torch.cat([ehs, a], dim=1)
     out = ref.attention("x", h, ctx)
     gold = torch.from_numpy(gd[f"c{c}_l{l}_{mode}_out"])
+    assert torch.allclose(out, gold, atol=1e-5, rtol=1e-4), (out - gold).abs().max().item()
+
+
+EXT_CASES = [("self_c320_l48", 320, 200, 320, "early"), ("self_c640_l32", 640, 201, 640, "early"),
+             ("nd4_c320_6x8", 320, 210, 768, "mid"), ("nd4_c640_4x4", 640, 211, 768, "mid"),
+             ("mask_query_c640_l32", 640, 220, 768, "late"), ("mask_key_c320_l48", 320, 221, 768, "late")]
+
+
+@pytest.mark.parametrize("name,c,seed,ctx,level", EXT_CASES)
+def test_oracle_processor_ext_matches_reference(name, c, seed, ctx, level):
+    """oracle.unet_ref.processor_call vs the reference processor on its off-pipeline paths:
+    encoder_hidden_states=None (K / V from the projected query), 4-D input, attention masks."""
+    gd = np.load(G / "processor_ext.npz")
+    w, _ = mini_attention_weights(c, seed, ctx)
+    pw = synth_processor_weights(level, seed=seed)
+    h = torch.from_numpy(gd[name + "_h"])
+    mask = torch.from_numpy(gd[name + "_mask"]) if name + "_mask" in gd else None
+    ehs = None if name.startswith("self") else torch.from_numpy(np.load(G / "processor.npz")["ehs"])
+    audio = {level: torch.from_numpy(np.load(G / "processor.npz")["audio"])}
+    out = unet_ref.processor_call(w, pw, h, ehs, audio, level, mask=mask)
+    gold = torch.from_numpy(gd[name + "_out"])
+    assert out.shape == gold.shape
     assert torch.allclose(out, gold, atol=1e-5, rtol=1e-4), (out - gold).abs().max().item()
 
 

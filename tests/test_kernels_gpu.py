@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from clap2diffusion_amd import ops
+from tests import parity_log
 
 pytestmark = pytest.mark.gpu
 
@@ -22,7 +23,22 @@ def close(out, ref, tol_max=2e-2, tol_l2=5e-3):
     err = (out - ref)
     rel_l2 = (err.norm() / ref.norm().clamp_min(1e-12)).item()
     rel_max = (err.abs().max() / ref.abs().max().clamp_min(1e-12)).item()
+    parity_log.record(rel_l2=rel_l2, rel_max=rel_max, tol_l2=tol_l2, tol_max=tol_max)
     assert rel_l2 <= tol_l2 and rel_max <= tol_max, f"rel_l2={rel_l2:.3e} rel_max={rel_max:.3e}"
+
+
+@pytest.fixture
+def force_plan():
+    """Force the implicit-GEMM plan through c2d_set_plan_override for one test."""
+    held = []
+
+    def _force(tile, split):
+        fp = ops.force_plan(tile, split)
+        fp.__enter__()
+        held.append(fp)
+    yield _force
+    for fp in held:
+        fp.__exit__(None, None, None)
 
 
 def gen(*shape, seed=0, scale=1.0):
@@ -126,17 +142,16 @@ def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
     close(nchw(out), ref)
 
 
-# every tile configuration left in igemm.hip's kDmaTiles, forced through C2D_GEMM_TILE
-# (read per launch) and confirmed through c2d_conv2d_igemm_plan
+# every tile configuration left in igemm.hip's kDmaTiles, forced through
+# c2d_set_plan_override and confirmed through c2d_conv2d_igemm_plan
 DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3]
 
 
 @pytest.mark.parametrize("tile", DMA_TILE_IDS)
 @pytest.mark.parametrize("k,split", [(3, 1), (1, 1), (3, 2)])
-def test_every_dma_tile_forced(dev, monkeypatch, tile, k, split):
+def test_every_dma_tile_forced(dev, force_plan, tile, k, split):
     n, h, cin, cout = 4, 16, 320, 640
-    monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
-    monkeypatch.setenv("C2D_GEMM_SPLIT", str(split))
+    force_plan(tile, split)
     x = gen(n, cin, h, h, seed=91)
     w = gen(cout, cin, k, k, seed=92, scale=1.0 / math.sqrt(k * k * cin))
     b = gen(cout, seed=93)
@@ -157,13 +172,12 @@ def test_every_dma_tile_forced(dev, monkeypatch, tile, k, split):
     (320, False, True, False),   # residual without a bias (zero bias in the image write)
     (320, True, False, True),    # time embedding alone
 ])
-def test_epilogue_operand_forms(dev, monkeypatch, tile, cout, temb, resid, bias):
+def test_epilogue_operand_forms(dev, force_plan, tile, cout, temb, resid, bias):
     """The epilogue forms (epilogue.h: workgroup image on the ping-pong tiles, per-wave
     prefetch on the 16x16 DMA family, compact / plain loops) on a ragged M (2 x 13 x 17
     pixels: partial row tiles, rows straddling images) against torch fp32."""
     n, h, w_, cin = 2, 13, 17, 320
-    monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
-    monkeypatch.setenv("C2D_GEMM_SPLIT", "1")
+    force_plan(tile, 1)
     x = gen(n, cin, h, w_, seed=111)
     w = gen(cout, cin, 3, 3, seed=112, scale=1.0 / math.sqrt(9 * cin))
     b = gen(cout, seed=113) if bias else None
@@ -185,10 +199,9 @@ def test_epilogue_operand_forms(dev, monkeypatch, tile, cout, temb, resid, bias)
 
 
 @pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 40)])   # odd column tiles: no GEGLU
-def test_every_dma_tile_forced_geglu(dev, monkeypatch, tile):
+def test_every_dma_tile_forced_geglu(dev, force_plan, tile):
     m, cin, inner = 1024, 320, 640
-    monkeypatch.setenv("C2D_GEMM_TILE", str(tile))
-    monkeypatch.setenv("C2D_GEMM_SPLIT", "1")
+    force_plan(tile, 1)
     x = gen(m, cin, seed=95)
     w = gen(2 * inner, cin, seed=96, scale=1.0 / math.sqrt(cin))
     b = gen(2 * inner, seed=97)
@@ -434,6 +447,34 @@ def test_attention_key_bias(dev, b, h, lq, lk, d, form):
     kh = k.view(b, lk, h, d).transpose(1, 2)
     vh = v.view(b, lk, h, d).transpose(1, 2)
     ref = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=bias[:, :, None, :]).transpose(1, 2).reshape(b * lq, h * d)
+    out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d,
+                        key_bias=bias.to(dev))
+    close(out, ref)
+
+
+@pytest.mark.parametrize("b,h,lq,lk,d,form", [
+    (2, 8, 300, 77, 40, "per_query"),       # [B, H, Lq, Lk] (resident K/V), ragged query tail
+    (1, 8, 200, 77, 80, "bh_flat"),         # [1, 1, Lq, Lk] broadcast over images and heads
+    (2, 4, 256, 333, 160, "per_query"),     # streaming K/V, masked key tail
+    (2, 8, 300, 77, 40, "neg_inf"),         # SDPA-style -inf entries, every row keeps a finite score
+])
+def test_attention_query_mask(dev, b, h, lq, lk, d, form):
+    """c2d_attention_fwd_mask: an attention_mask varying over queries, as the reference
+    processor hands it to get_attention_scores (models/audio_attention_processor.py:129)."""
+    q, k, v = gen(b * lq, h * d, seed=71), gen(b * lk, h * d, seed=72), gen(b * lk, h * d, seed=73)
+    g = torch.Generator().manual_seed(74)
+    if form == "bh_flat":
+        bias = torch.randn(1, 1, lq, lk, generator=g) * 3.0
+    else:
+        bias = torch.randn(b, h, lq, lk, generator=g) * 2.0
+    if form == "neg_inf":
+        drop = torch.rand(b, h, lq, lk, generator=g) < 0.4
+        drop[..., 5] = False
+        bias = bias.masked_fill(drop, float("-inf"))
+    qh = q.view(b, lq, h, d).transpose(1, 2)
+    kh = k.view(b, lk, h, d).transpose(1, 2)
+    vh = v.view(b, lk, h, d).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=bias).transpose(1, 2).reshape(b * lq, h * d)
     out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d,
                         key_bias=bias.to(dev))
     close(out, ref)

@@ -68,7 +68,10 @@ def test_product_crop_matches_reference_truncation():
     fe.max_len = 4
     x = np.arange(10, dtype=np.float32)
     np.random.seed(0)
-    a = fe.crop([x, x[:2], np.stack([x, x], 1)])
+    a = fe.crop([x, x[:2], np.stack([x, x], 1), np.zeros(0, np.float32)])
     np.testing.assert_array_equal(a[0], [0, 1, 2, 3])
     np.testing.assert_array_equal(a[1], [0, 1])
     np.testing.assert_array_equal(a[2], [0, 1, 2, 3])
+    # an empty clip passes through (length 0): the kernel zero-pads it to max_len samples of
+    # silence, as the reference's preprocess_audio zero-pads (models/audio_encoder.py:123-126)
+    assert a[3].size == 0

@@ -67,3 +67,17 @@ def test_log_mel_silence_floor(dev):
     fe = ClapLogMel(dev, max_length_s=1)
     out = fe([np.zeros(48_000, np.float32)]).cpu()
     assert torch.all((out + 100.0).abs() < 1e-4)
+
+
+def test_log_mel_empty_clip_is_silence(dev):
+    # the reference zero-pads an empty clip to max_len samples (models/audio_encoder.py:123-126):
+    # log-mel of silence (-100 dB), beside a real clip and alone
+    from clap2diffusion_amd.features import ClapLogMel
+    from oracle.mel_ref import log_mel
+    fe = ClapLogMel(dev, max_length_s=1)
+    c = np.random.RandomState(3).randn(30_000).astype(np.float32) * 0.1
+    out = fe([np.zeros(0, np.float32), c]).cpu().numpy()
+    assert np.all(np.abs(out[0] + 100.0) < 1e-4)
+    assert np.abs(out[1] - log_mel(c, max_len=48_000)).max() < TOL_DB
+    alone = fe([np.zeros(0, np.float32)]).cpu().numpy()
+    assert np.all(np.abs(alone + 100.0) < 1e-4)

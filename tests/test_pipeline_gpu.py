@@ -10,6 +10,7 @@ import torch
 from clap2diffusion_amd.pipeline import AudioToImageInference, initial_latents, synthetic_thunder
 from clap2diffusion_amd.text_encoder import tokenize
 from oracle.pipeline_ref import ReferencePipeline, reference_images
+from tests import parity_log
 
 pytestmark = pytest.mark.gpu
 
@@ -24,6 +25,14 @@ def psnr(a, b):
     return 99.0 if mse == 0 else 10 * math.log10(255.0 ** 2 / mse)
 
 
+def image_parity(img, ref, psnr_min, mad_max=3.0, **extra):
+    """PSNR / mean |diff| (uint8 units) of HIP vs oracle images, recorded, then asserted."""
+    p = psnr(img, ref)
+    mad = (img.float() - ref.float()).abs().mean().item()
+    parity_log.record(psnr_db=p, mean_abs_diff=mad, psnr_min=psnr_min, mad_max=mad_max, **extra)
+    assert p >= psnr_min and mad <= mad_max, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+
+
 def test_pipeline_matches_oracle_10_steps(pipe, dev):
     b = 2
     mel = pipe.mel_features([synthetic_thunder(i) for i in range(b)])
@@ -33,10 +42,9 @@ def test_pipeline_matches_oracle_10_steps(pipe, dev):
     lat_hip = pipe.last_denoiser.x.cpu()
     ref, lat_ref = reference_images(mel.cpu(), ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10)
     rel = ((lat_hip - lat_ref).norm() / lat_ref.norm()).item()
-    p = psnr(img, ref)
-    mad = (img.float() - ref.float()).abs().mean().item()
+    parity_log.record(latent_rel_l2=rel, tol_l2=2e-2)
     assert rel < 2e-2, f"final latent rel-L2 {rel:.3e}"
-    assert p >= 30.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+    image_parity(img, ref, 30.0)
 
 
 def test_pipeline_matches_oracle_50_steps_batch1(pipe, dev):
@@ -46,9 +54,7 @@ def test_pipeline_matches_oracle_50_steps_batch1(pipe, dev):
     lat = pipe.initial_latents([9])
     img = pipe.generate_batch(mel, None, 50, 7.5, ids=ids, latents=lat).cpu()
     ref, _ = reference_images(mel.cpu(), ids[0].cpu(), ids[1].cpu(), lat.cpu(), 50)
-    p = psnr(img, ref)
-    mad = (img.float() - ref.float()).abs().mean().item()
-    assert p >= 25.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+    image_parity(img, ref, 25.0)
 
 
 def test_graph_replay_is_repeatable(pipe, dev):
@@ -86,9 +92,7 @@ def test_c1_workload_512_10_steps_from_waveform(pipe, dev):
     img = pipe.generate_batch(mel, None, 10, 7.5, ids=ids, latents=lat).cpu()
     assert img.shape == (1, 512, 512, 3)
     ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10)
-    p = psnr(img, ref)
-    mad = (img.float() - ref.float()).abs().mean().item()
-    assert p >= 30.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+    image_parity(img, ref, 30.0)
 
 
 @pytest.mark.timeout(900)
@@ -103,9 +107,7 @@ def test_c5_shape_768_from_waveform(pipe, dev):
     img = pipe.generate_batch(mel, None, 3, 7.5, ids=ids, latents=lat).cpu()
     assert img.shape == (1, 768, 768, 3)
     ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 3)
-    p = psnr(img, ref)
-    mad = (img.float() - ref.float()).abs().mean().item()
-    assert p >= 30.0 and mad <= 3.0, f"PSNR {p:.2f} dB, mean|diff| {mad:.2f}"
+    image_parity(img, ref, 30.0)
 
 
 def test_clap_encoder_checkpoint_is_loaded(dev, tmp_path):
@@ -176,3 +178,38 @@ def test_sd15_folder_weights_drive_the_pipeline(dev, tmp_path):
     ia = a.generate_batch(mel, None, 5, 7.5, ids=ids, latents=lat).cpu()
     ib = b.generate_batch(mel, None, 5, 7.5, ids=ids, latents=lat).cpu()
     assert (ia.int() - ib.int()).abs().max().item() <= 1
+
+
+@pytest.mark.timeout(1200)
+def test_bench_c3_exact_workload_graphed_vs_eager_and_oracle(dev):
+    """What bench.py times, checked: config c3 (B = 8, 512^2, 50 DDIM steps, CFG 7.5) on the
+    bench's own inputs (distributed.rank_inputs(range(8), (64, 64)): synthetic thunder clips,
+    bench prompts, per-sample seeded latents) through generate_batch_graphed, the BatchGraph
+    the bench replays.  (1) Bit-identical to the eager generate_batch on the same inputs
+    (images and final latents).  (2) Sample 0 against the fp32 oracle pipeline at 50 steps
+    (oracle.pipeline_ref.ReferencePipeline: log-mel -> HTSAT -> projectors -> CLIP -> 50
+    CFG-pair UNet calls -> VAE): PSNR >= 25 dB, mean |diff| <= 3/255."""
+    import numpy as np
+    from clap2diffusion_amd import distributed as D
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    pipe = AudioToImageInference(device=dev, height=512, width=512, verbose=False)
+    inp = D.rank_inputs(list(range(8)), (64, 64), dev)
+    clips = pipe.feature_extractor.crop(inp.audios)
+    wave = torch.from_numpy(np.concatenate(clips)).to(dev)
+    lens = torch.tensor([c.size for c in clips], dtype=torch.int32, device=dev)
+    offs = torch.tensor(np.cumsum([0] + [c.size for c in clips[:-1]]), dtype=torch.int64, device=dev)
+    ids = (inp.ids_uncond, inp.ids_cond)
+    g = pipe.generate_batch_graphed(wave, offs, lens, ids, inp.latents, 50, 7.5).clone()
+    lat_g = pipe.last_denoiser.x.clone()
+    g2 = pipe.generate_batch_graphed(wave, offs, lens, ids, inp.latents, 50, 7.5).clone()   # a second replay
+    e = pipe.generate_batch(pipe.feature_extractor.from_device(wave, offs, lens), None, 50, 7.5, ids=ids,
+                            latents=inp.latents)
+    lat_e = pipe.last_denoiser.x.clone()
+    assert g.shape == (8, 512, 512, 3)
+    assert torch.equal(g, g2), "BatchGraph replay is not repeatable"
+    assert torch.equal(g, e) and torch.equal(lat_g, lat_e), "BatchGraph != eager pipeline"
+    parity_log.record(graphed_vs_eager="bit-identical", images=8)
+    ref, lat_ref = ReferencePipeline(0).run([inp.audios[0]], inp.ids_uncond[:1].cpu(), inp.ids_cond[:1].cpu(),
+                                            inp.latents[:1].cpu(), 50)
+    rel = ((lat_g[:1].cpu() - lat_ref).norm() / lat_ref.norm()).item()
+    image_parity(g[:1].cpu(), ref, 25.0, latent_rel_l2=rel)

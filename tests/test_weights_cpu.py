@@ -53,3 +53,45 @@ def test_weights_files_and_sd15_folder(tmp_path):
     assert out["vae"][a + "to_out.0.weight"].shape == (512, 512)
     assert torch.equal(out["vae"][a + "to_out.0.weight"], vae[a + "proj_attn.weight"][:, :, 0, 0])
     assert torch.equal(out["text_encoder"]["text_model.final_layer_norm.weight"], torch.ones(768))
+
+
+def test_clap_weight_precedence(tmp_path):
+    """An explicit --clap_model file wins over checkpoint_dir/clap_encoder.pth; an unrecognised
+    clap_encoder.pth is reported and skipped (the reference carries on); neither -> seeded."""
+    import pytest
+    ck = tmp_path / "ck"
+    ck.mkdir()
+    explicit = tmp_path / "clap.pth"
+    torch.save(W.synth_htsat(5), explicit)
+    torch.save({"clap_model." + k: v for k, v in W.synth_htsat(6).items()}, ck / "clap_encoder.pth")
+    sd, src = W.resolve_clap_weights(ck, explicit, seed=0)
+    k = "audio_projection.linear1.weight" if "audio_projection.linear1.weight" in sd else next(iter(sd))
+    assert torch.equal(sd[k], W.synth_htsat(5)[k]) and "--clap_model" in src
+    sd, src = W.resolve_clap_weights(ck, None, seed=0)
+    assert torch.equal(sd[k], W.synth_htsat(6)[k]) and src.endswith("clap_encoder.pth")
+    torch.save({"something_else.weight": torch.zeros(3)}, ck / "clap_encoder.pth")
+    with pytest.warns(UserWarning, match="no CLAP audio-tower keys"):
+        sd, src = W.resolve_clap_weights(ck, None, seed=2)
+    assert torch.equal(sd[k], W.synth_htsat(2)[k]) and "seeded" in src
+    sd, src = W.resolve_clap_weights(tmp_path / "nowhere", None, seed=1)
+    assert torch.equal(sd[k], W.synth_htsat(1)[k])
+
+
+def test_processor_checkpoint_forms():
+    """unet_adapter_final.pth forms -> per-level AudioAttnProcessor state dicts."""
+    mapping = {"early": ["down_blocks.0.attentions.0.transformer_blocks.0.attn2.processor"],
+               "mid": ["mid_block.attentions.0.transformer_blocks.0.attn2.processor"],
+               "late": ["up_blocks.1.attentions.2.transformer_blocks.0.attn2.processor"]}
+    per = {lv: W.synth_processor_weights(lv, seed=i) for i, lv in enumerate(("early", "mid", "late"))}
+    forms = [per, {"state_dict": per},
+             {f"{lv}.{k}": v for lv, sd in per.items() for k, v in sd.items()},
+             {f"processors.{lv}.{k}": v for lv, sd in per.items() for k, v in sd.items()},
+             {f"{mapping[lv][0]}.{k}": v for lv, sd in per.items() for k, v in sd.items()}]
+    for ck in forms:
+        got = W.processor_state_dicts(ck, mapping)
+        assert set(got) == {"early", "mid", "late"}, list(ck)[:3]
+        for lv in got:
+            assert all(torch.equal(got[lv][k], per[lv][k]) for k in W.PROCESSOR_KEYS)
+    one = W.processor_state_dicts(per["mid"], mapping)   # a single processor for every level
+    assert set(one) == {"early", "mid", "late"} and torch.equal(one["early"]["alpha"], per["mid"]["alpha"])
+    assert W.processor_state_dicts({"foo.weight": torch.zeros(2)}, mapping) == {}
