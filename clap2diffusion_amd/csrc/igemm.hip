@@ -866,7 +866,18 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act) {
     // the plain (per-wave image) epilogue
     const int t256x320 = (geglu || !C2D_PP16_DEFAULT) ? 25 : 40;
     const long t24 = ((M + 255) / 256) * ((cout + 319) / 320);
-    if (t24 >= 192) return {t256x320, 1, nk};
+    if (t24 >= 192) {
+        // 256 x 256 (tile 41) where its round count x tile width is smaller: the partial last
+        // round of the 320-wide tiles costs a whole round (scripts/ab_tiles.py, same box:
+        // L1 QKV 640 -> 1920 64.8 -> 57.8 us, L2 QKV 1280 -> 3840 54.0 -> 48.0 us; L0 QKV and
+        // every 320 / 640-wide conv keep tile 40 by the same count)
+        if (!geglu && C2D_PP16_DEFAULT) {
+            const long mt = (M + 255) / 256;
+            const long r40 = (t24 + 255) / 256, r41 = (mt * ((cout + 255) / 256) + 255) / 256;
+            if (r41 * 256 < r40 * 320) return {41, 1, nk};
+        }
+        return {t256x320, 1, nk};
+    }
     if (nk >= 90 && t24 >= 64) {
         DmaPlan pl = plan_dma(M, cout, nk, geglu, 25, 0);
         if (pl.id == 25) pl.id = t256x320;

@@ -131,6 +131,13 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
 #undef C2D_BAR
 
     const int mw0 = m0 + wr * TMW * 16, nw0 = n0 + wc * TN * 16;
+    if (C2D_ABL(p.abl, 4)) {   // timing ablation: no epilogue (accumulators kept live)
+#pragma unroll
+        for (int a = 0; a < TN; ++a)
+#pragma unroll
+            for (int b = 0; b < TMW; ++b) asm volatile("" :: "v"(acc[a][b]));
+        return;
+    }
     if (p.ksplit > 1) {
         float* dst = p.ws + (size_t)slice * p.M * p.cout;
 #pragma unroll

@@ -21,7 +21,9 @@ blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
   Normalised activations are materialised once per norm (HBM-bound kernels):
   re-normalising inside the consumer GEMM would redo the affine+SiLU in all 9
   taps of a 3x3 conv / every N-tile of a GEMM, which is VALU-bound on CDNA4.
-  Up/Downsample   nearest-x2 gather and stride-2 folded into the conv addressing.
+  Up/Downsample   stride 2 folded into the conv addressing; the nearest x2 upsample
+                  materialised by c2d_upsample_nearest2x (one HBM pass) so the 3x3 conv
+                  stays on the LDS-DMA path (Upsample2D below).
 """
 from __future__ import annotations
 

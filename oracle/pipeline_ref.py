@@ -51,9 +51,10 @@ class ReferencePipeline:
 
     @torch.no_grad()
     def run(self, mel_or_waves, ids_uncond: torch.Tensor, ids_cond: torch.Tensor, latents: torch.Tensor,
-            steps: int, guidance: float = 7.5, timings: dict | None = None):
+            steps: int, guidance: float = 7.5, timings: dict | None = None, progress=None):
         """-> (uint8 NHWC images, final latents).  timings (optional dict) receives the
-        seconds spent per stage: mel, condition, unet (list, one per CFG-pair call), vae."""
+        seconds spent per stage: mel, condition, unet (list, one per CFG-pair call), vae;
+        progress (optional callable) gets a short string after every UNet call."""
         tm = timings if timings is not None else {}
         t0 = time.perf_counter()
         mel = mel_or_waves if isinstance(mel_or_waves, torch.Tensor) else self.mel(mel_or_waves)
@@ -69,6 +70,8 @@ class ReferencePipeline:
             eu, ec = eps.chunk(2)
             x = ddim_step(eu + guidance * (ec - eu), int(t), x, steps, ac)
             tm["unet"].append(time.perf_counter() - ts)
+            if progress is not None:
+                progress(f"oracle step {len(tm['unet'])}/{steps} t={int(t)} {tm['unet'][-1]:.1f}s")
         t3 = time.perf_counter()
         img = self.vae(x)
         t4 = time.perf_counter()

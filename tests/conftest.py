@@ -27,3 +27,17 @@ def dev():
     from clap2diffusion_amd import _lib
     _lib.lib()  # loud failure if the library is missing
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def progress():
+    """Append a line to gpurun_out/test_progress.log (long CPU-oracle legs of the GPU tests keep
+    the GPU box's output alive: pytest captures stdout / stderr until a test ends)."""
+    import time
+    path = ROOT / "gpurun_out" / "test_progress.log"
+    path.parent.mkdir(parents=True, exist_ok=True)
+
+    def _log(msg: str) -> None:
+        with open(path, "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {os.environ.get('PYTEST_CURRENT_TEST', '?').split(' ')[0]} {msg}\n")
+    return _log

@@ -81,7 +81,7 @@ def test_reference_api_surface(pipe, tmp_path):
 
 
 @pytest.mark.timeout(900)
-def test_c1_workload_512_10_steps_from_waveform(pipe, dev):
+def test_c1_workload_512_10_steps_from_waveform(pipe, dev, progress):
     # BASELINE.json c1's workload (1 x 512^2, 10 DDIM steps, "Thunder" + "a beach") end to end
     # from the 48 kHz waveform: HIP log-mel -> ... -> VAE against the fp32 oracle pipeline
     # (oracle log-mel from the same waveform): PSNR >= 30 dB, mean |diff| <= 3/255
@@ -91,12 +91,12 @@ def test_c1_workload_512_10_steps_from_waveform(pipe, dev):
     lat = initial_latents([0], 64, 64, dev)
     img = pipe.generate_batch(mel, None, 10, 7.5, ids=ids, latents=lat).cpu()
     assert img.shape == (1, 512, 512, 3)
-    ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10)
+    ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10, progress=progress)
     image_parity(img, ref, 30.0)
 
 
 @pytest.mark.timeout(900)
-def test_c5_shape_768_from_waveform(pipe, dev):
+def test_c5_shape_768_from_waveform(pipe, dev, progress):
     # BASELINE.json c5's shape (768^2 = 96^2 latent: 9216-key self-attention, 48^2 / 24^2 / 12^2
     # levels) end to end from the waveform, 3 DDIM steps (the oracle UNet at 96^2 takes ~10 s
     # per CFG-pair call): PSNR >= 30 dB, mean |diff| <= 3/255
@@ -106,7 +106,7 @@ def test_c5_shape_768_from_waveform(pipe, dev):
     lat = initial_latents([4], 96, 96, dev)
     img = pipe.generate_batch(mel, None, 3, 7.5, ids=ids, latents=lat).cpu()
     assert img.shape == (1, 768, 768, 3)
-    ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 3)
+    ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 3, progress=progress)
     image_parity(img, ref, 30.0)
 
 
@@ -181,7 +181,7 @@ def test_sd15_folder_weights_drive_the_pipeline(dev, tmp_path):
 
 
 @pytest.mark.timeout(1200)
-def test_bench_c3_exact_workload_graphed_vs_eager_and_oracle(dev):
+def test_bench_c3_exact_workload_graphed_vs_eager_and_oracle(dev, progress):
     """What bench.py times, checked: config c3 (B = 8, 512^2, 50 DDIM steps, CFG 7.5) on the
     bench's own inputs (distributed.rank_inputs(range(8), (64, 64)): synthetic thunder clips,
     bench prompts, per-sample seeded latents) through generate_batch_graphed, the BatchGraph
@@ -209,7 +209,8 @@ def test_bench_c3_exact_workload_graphed_vs_eager_and_oracle(dev):
     assert torch.equal(g, g2), "BatchGraph replay is not repeatable"
     assert torch.equal(g, e) and torch.equal(lat_g, lat_e), "BatchGraph != eager pipeline"
     parity_log.record(graphed_vs_eager="bit-identical", images=8)
+    progress("graphed == eager (8 images, 50 steps); fp32 oracle for sample 0")
     ref, lat_ref = ReferencePipeline(0).run([inp.audios[0]], inp.ids_uncond[:1].cpu(), inp.ids_cond[:1].cpu(),
-                                            inp.latents[:1].cpu(), 50)
+                                            inp.latents[:1].cpu(), 50, progress=progress)
     rel = ((lat_g[:1].cpu() - lat_ref).norm() / lat_ref.norm()).item()
     image_parity(g[:1].cpu(), ref, 25.0, latent_rel_l2=rel)
