@@ -680,6 +680,7 @@ __global__ void splitk_reduce_kernel(IgemmParams p);
 }  // namespace c2d
 #include "igemm_m32.h"
 #include "igemm_pp16.h"
+#include "igemm_pps.h"
 namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -732,10 +733,11 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 #define C2D_TILE_FN(ID) void run_tile_##ID(IgemmParams& p, int ksize, int cout, hipStream_t s)
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
-C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3);
+C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50);
 #if C2D_PART(1)
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
+C2D_TILE_FN(50) { (void)ksize; (void)cout; run_pps(p, s); }   // persistent 192x256, carried epilogue (1x1)
 #endif
 #if C2D_PART(2)
 C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
@@ -832,11 +834,31 @@ static int gemm_split() { return plan_override_split(); }
 // GEMMs, the GEGLU projections, the 256-row-tile-rich up-block convs); otherwise
 // the 128x320 tile (id 7; GEGLU: 256x128, id 1) when its tiles fill the chip;
 // under-filled shapes (16x16 / 8x8 levels) go through the cost model with split-K.
-static DmaPlan plan_for(long M, int cout, int kpad, int act) {
+// the persistent carried-epilogue kernel (tile 50, igemm_pps.h): 1x1, plain output (no
+// residual / time embedding, act none or GEGLU), K = 320 / 640 / 1280, 8-B aligned output,
+// 32-bit buffer offsets
+static bool pps_eligible(const c2d_conv_desc* d) {
+    const long M = (long)d->n * d->oh * d->ow;
+    return d->ksize == 1 && !d->resid && !d->temb && (d->act == C2D_ACT_NONE || d->act == C2D_ACT_GEGLU) &&
+           pps_nk_ok(d->kpad / 64) && (d->out_ld % 4) == 0 && ((uintptr_t)d->out & 7) == 0 &&
+           ((uintptr_t)d->bias & 15) == 0 && (size_t)M * d->out_ld * 2 < (1u << 31);
+}
+
+static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok) {
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
     int id = gemm_tile();
     if (id == 7 && geglu) id = 0;
+    if (id == 50) {
+        if (pps_ok) return {50, 1, nk};
+        id = 0;
+    }
+    // GEGLU with K = 320 / 640 on the chip-filling grids: the persistent carried-epilogue
+    // kernel (same box, scripts/ab_tiles.py: L0 320 -> 2 x 1280 187 -> 166 us, L1 640 -> 2 x 2560
+    // 147 -> 138 us; K = 1280 and the plain outputs stay on the one-shot tiles, where its
+    // 192 x 256 tile's extra DMA per MAC costs more than the overlap saves)
+    if (!id && pps_ok && geglu && (nk == 5 || nk == 10) && ((M + 191) / 192) * ((cout + 255) / 256) >= 512)
+        return {50, 1, nk};
     if (id) {
         DmaPlan pl = plan_dma(M, cout, nk, geglu, id, gemm_split());
         if (pl.id) return pl;
@@ -897,6 +919,7 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 41: return run_tile_41(p, ksize, cout, s);
         case 28: return run_tile_28(p, ksize, cout, s);
         case 29: return run_tile_29(p, ksize, cout, s);
+        case 50: return run_tile_50(p, ksize, cout, s);
         case 7: return run_tile_7(p, ksize, cout, s);
         case 1: return run_tile_1(p, ksize, cout, s);
         case 2: return run_tile_2(p, ksize, cout, s);
@@ -918,7 +941,7 @@ extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
     if (!dma_eligible(d)) return 0;
     const long M = (long)d->n * d->oh * d->ow;
-    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act);
+    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d));
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
 
@@ -931,7 +954,7 @@ extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* 
         return C2D_OK;
     }
     const long M = (long)d->n * d->oh * d->ow;
-    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act);
+    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d));
     if (pl.split > 1) {
         const size_t need = (size_t)pl.split * M * d->cout * sizeof(float);
         if (!(d->ws && d->ws_bytes >= need && aligned16(d->ws))) pl.split = 1;
@@ -997,7 +1020,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act);
+        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d));
         if (pl.split > 1) {
             const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
             if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {

@@ -69,11 +69,13 @@ class GraphDenoiser:
             self.context_kv[attn] = attn.processor.context_kv(attn, self.ehs, audio, out=buf)
 
     def _body(self) -> None:
-        xin = ops.latent_to_nhwc(self.x, self.unet.in_pad, dup=True)
+        # the CFG pair [x; x] enters the UNet as x once (forward_nhwc cfg_pair: the prefix before
+        # the first cross-attention runs on one half and is duplicated there)
+        xin = ops.latent_to_nhwc(self.x, self.unet.in_pad, dup=False)
         torch.index_select(self.temb_table, 0, self.step_idx, out=self.temb_cur)
         temb_all = self.temb_cur.expand(2 * self.b, self.temb_cur.shape[1])   # zero row stride: one row for all
         eps = self.unet.forward_nhwc(xin, None, self.ehs, dict(self.kw, context_kv=self.context_kv),
-                                     temb_all=temb_all)
+                                     temb_all=temb_all, cfg_pair=True)
         ops.cfg_ddim_step(eps, self.x, self.g, self.coef, self.step_idx, advance=True)
 
     def capture(self) -> None:

@@ -138,11 +138,16 @@ class BasicTransformerBlock(nn.Module):
         return ops.add(out.to(h.dtype).contiguous(), h)
 
     def forward(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict,
-                encoder_attention_mask: torch.Tensor | None = None) -> torch.Tensor:
+                encoder_attention_mask: torch.Tensor | None = None, cfg_dup: bool = False) -> torch.Tensor:
         """h: [B, L, C] fp16 (updated in place by the fused residual epilogues).
-        encoder_attention_mask: additive key bias for attn2 (diffusers BasicTransformerBlock)."""
+        encoder_attention_mask: additive key bias for attn2 (diffusers BasicTransformerBlock).
+        cfg_dup: h holds one half of a CFG pair whose halves are identical up to here; the
+        self-attention runs on it once and the result is duplicated before attn2, the first
+        op where the [uncond, cond] halves differ (UNet2DConditionModel.forward_nhwc)."""
         kw = cross_attention_kwargs or {}
         h = self._attend(self.attn1, self.norm1(h), h, None, None, kw)
+        if cfg_dup:
+            h = torch.cat([h, h], 0)
         h = self._attend(self.attn2, self.norm2(h), h, ehs, encoder_attention_mask, kw)
         b, l, c = h.shape
         h2 = h.view(b * l, c)
@@ -159,10 +164,15 @@ class Transformer2DModel(nn.Module):
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(c, heads, cross_dim)])
         self.proj_out = HConv2d(c, c, 1)
 
-    def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None):
+    def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None, cfg_dup: bool = False):
+        """cfg_dup: x is one half of a CFG pair with identical halves; the output is the full
+        pair (the block duplicates its state before the cross-attention)."""
         n, hh, ww, c = x.shape
         h = self.proj_in(self.norm.apply(x))
-        t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
+        t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
+                                       cfg_dup=cfg_dup)
+        if cfg_dup:
+            x, n = torch.cat([x, x], 0), 2 * n
         return self.proj_out(t.view(n, hh, ww, c), resid=x)
 
 
@@ -339,26 +349,47 @@ class UNet2DConditionModel(nn.Module):
         return ops.conv(temb, self.w_temb_all, self.temb_kpad, self.temb_total, ksize=1, bias=self.b_temb_all,
                         silu_in=True)
 
+    def cfg_shared_prefix_ok(self) -> bool:
+        """The [uncond, cond] halves of a CFG batch see the same latent, timestep and (per the
+        composition contract) audio tokens; they first differ at the first cross-attention,
+        where the text context enters (down_blocks.0.attentions.0...attn2).  Everything before
+        it -- conv_in, the first ResnetBlock2D, that transformer's GroupNorm, proj_in, LayerNorm
+        and self-attention -- can run on one half and be duplicated, when the self-attention
+        there runs the stock processor (a plugin on attn1 may use per-half kwargs)."""
+        blk = self.down_blocks[0]
+        if not len(blk.attentions):
+            return False
+        return type(blk.attentions[0].transformer_blocks[0].attn1.processor) is AttnProcessor
+
     def forward_nhwc(self, x: torch.Tensor, t_sin: torch.Tensor | None, ehs: torch.Tensor,
                      cross_attention_kwargs: dict | None = None,
                      encoder_attention_mask: torch.Tensor | None = None,
-                     temb_all: torch.Tensor | None = None) -> torch.Tensor:
+                     temb_all: torch.Tensor | None = None, cfg_pair: bool = False) -> torch.Tensor:
         """x: [N, H, W, 8] fp16 (latent zero-padded to 8 ch); t_sin: [N, 320] fp16
         sinusoidal embedding; ehs: [N, 77, 768] fp16; encoder_attention_mask: additive
         key bias [N, 1, 77] for every attn2 (or None); temb_all: precomputed
         time_conditioning rows [N, 22 x cout] (any row stride, 0 = one row for all) in place
-        of t_sin. Returns eps [N, H, W, 4] fp16."""
+        of t_sin.  cfg_pair: x holds N/2 latents and the UNet batch is the CFG pair [x; x]
+        (the prefix before the first cross-attention then runs once per latent,
+        cfg_shared_prefix_ok); t_sin / temb_all rows must then be the same for both halves.
+        Returns eps [N, H, W, 4] fp16."""
         kw = cross_attention_kwargs or {}
         em = encoder_attention_mask
         if temb_all is None:
             temb_all = self.time_conditioning(t_sin)
+        shared = cfg_pair and self.cfg_shared_prefix_ok()
+        if cfg_pair and not shared:
+            x = torch.cat([x, x], 0)
         h = self.conv_in(x)
-        skips = [h]
-        for blk in self.down_blocks:
+        skips = [torch.cat([h, h], 0) if shared else h]
+        for i, blk in enumerate(self.down_blocks):
             for j, r in enumerate(blk.resnets):
+                pre = shared and i == 0 and j == 0   # still on one half of the CFG pair
                 h = r(h, temb_all)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw, em)
+                    h = blk.attentions[j](h, ehs, kw, em, cfg_dup=pre)
+                elif pre:
+                    h = torch.cat([h, h], 0)
                 skips.append(h)
             if hasattr(blk, "downsamplers"):
                 h = blk.downsamplers[0](h)

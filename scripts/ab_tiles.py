@@ -23,6 +23,9 @@ SHAPES = {
     "qkv0": (1, 64, 320, 960, None, 16, False),
     "qkv1": (1, 32, 640, 1920, None, 16, False),
     "qkv2": (1, 16, 1280, 3840, None, 16, False),
+    "toq0": (1, 64, 320, 320, None, 16, False),
+    "toq1": (1, 32, 640, 640, None, 16, False),
+    "toq2": (1, 16, 1280, 1280, None, 16, False),
     "proj0": (1, 64, 320, 320, None, 16, True),
     "proj1": (1, 32, 640, 640, None, 16, True),
     "proj2": (1, 16, 1280, 1280, None, 16, True),

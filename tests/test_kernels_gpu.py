@@ -165,6 +165,36 @@ def test_every_dma_tile_forced(dev, force_plan, tile, k, split):
     close(nchw(out), ref)
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,act,bias", [
+    (3, 61, 61, 320, 2560, "geglu", True),    # K = 320 (5 K steps), 590 tiles: several per workgroup, ragged M
+    (16, 64, 64, 320, 960, None, False),      # the L0 QKV shape, 342 x 4 tiles, no bias
+    (4, 37, 41, 640, 1280, None, True),       # K = 640, 160 tiles (< one per CU), ragged M
+    (2, 50, 50, 1280, 2560, "geglu", True),   # K = 1280 (20 K steps), 270 tiles
+    (1, 9, 7, 320, 768, None, True),          # a single partial tile
+])
+def test_persistent_carried_epilogue_gemm(dev, force_plan, n, h, w, cin, cout, act, bias):
+    """Tile 50 (igemm_pps.h): the persistent 192 x 256 ping-pong 1x1 GEMM whose epilogue
+    (bias, GEGLU h * gelu(g), fp16 stores) rides in the next tile's K loop, against torch fp32
+    (GEGLU with the exact erf GELU: the kernel's sigmoid-form GELU is within 3.4e-5)."""
+    force_plan(50, 0)
+    x = gen(n, cin, h, w, seed=131)
+    wt = gen(cout, cin, 1, 1, seed=132, scale=1.0 / math.sqrt(cin))
+    b = gen(cout, seed=133) if bias else None
+    ref = F.conv2d(x, wt, b)
+    wp, kp = ops.pack_conv_weight(wt)
+    bd = b.float().to(dev) if bias else None
+    if act == "geglu":
+        wi, bi = ops.geglu_interleave(wt[:, :, 0, 0], b)
+        wp, kp = ops.pack_linear_weight(wi)
+        bd = bi.float().to(dev) if bias else None
+        hh, gg = ref.chunk(2, dim=1)
+        ref = hh * F.gelu(gg)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(nhwc(x).half().to(dev), wp.to(dev), kp, cout, ksize=1, bias=bd, act=act)
+    assert plans == [(50, 1)], plans
+    close(nchw(out), ref)
+
+
 @pytest.mark.parametrize("tile", DMA_TILE_IDS)
 @pytest.mark.parametrize("cout,temb,resid,bias", [
     (336, True, True, True),     # 16-B (W = 8) form, every operand, ragged last column tile

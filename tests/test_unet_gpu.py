@@ -127,6 +127,29 @@ def test_unet_step_c5_batch_matches_oracle(dev, unet_pair):
     assert err <= 1e-2, f"eps rel-L2 {err:.3e}"
 
 
+@pytest.mark.parametrize("n,hw", [(16, 64), (2, 32)])
+def test_cfg_shared_prefix_matches_full_pair(dev, unet_pair, n, hw):
+    """forward_nhwc(cfg_pair=True): the layers before the first cross-attention run on one
+    half of the CFG batch and are duplicated there -- the same eps as the duplicated input
+    through the whole UNet (equal up to the accumulation order of the half-size GEMM plans)."""
+    hip, ref, mgr = unet_pair
+    g = torch.Generator().manual_seed(77 + n)
+    b = n // 2
+    x = torch.randn(b, 4, hw, hw, generator=g)
+    ehs = torch.randn(n, 77, 768, generator=g).to(dev, torch.float16)
+    audio = {lv: torch.randn(n, 10, 768, generator=g).to(dev, torch.float16) * 0.5 for lv in ("early", "mid", "late")}
+    kw = mgr.get_audio_kwargs(audio)
+    t_sin = ops.timestep_embedding(torch.tensor([501.0], device=dev), None, n, 320)
+    with torch.no_grad():
+        xin = ops.latent_to_nhwc(x.to(dev), hip.in_pad, dup=False)
+        e_shared = hip.forward_nhwc(xin, t_sin, ehs, kw, cfg_pair=True).float()
+        e_full = hip.forward_nhwc(torch.cat([xin, xin], 0), t_sin, ehs, kw).float()
+    assert hip.cfg_shared_prefix_ok()
+    err = rel_l2(e_shared, e_full, record=False)
+    parity_log.record(rel_l2=err, tol_l2=2e-3)
+    assert err <= 2e-3, err
+
+
 def test_unet_encoder_attention_mask_matches_oracle(dev, unet_pair):
     # diffusers' encoder_attention_mask (keep-mask [N, 77]) -> additive key bias on every attn2
     hip, ref, mgr = unet_pair
