@@ -105,6 +105,21 @@ __device__ __forceinline__ float erf_as(float x) {
 }
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f)); }
 
+// GELU of the GEGLU epilogues (gelu_f stays for C2D_ACT_GELU): x * sigmoid(z), z = x' (a + b x'^2 + c x'^4), x' = x
+// clamped to [-8, 8] (z monotone there; sigmoid(z(+-8)) is 1 / 0 to 1e-12).  Coefficients fitted
+// (near-minimax) to the erf form 0.5 x (1 + erf(x / sqrt 2)) diffusers' GEGLU uses: max
+// |error| 3.4e-5 over the real line, below the fp16 rounding of every GEGLU output above
+// 0.07 in magnitude; 7 VALU + 2 transcendental issue slots against ~17 + 2 for the
+// Abramowitz-Stegun erf (gelu_f), the op count the carried epilogue hides under the MFMAs.
+// log2(e) is folded into the coefficients (exp2 on the hardware unit).
+__device__ __forceinline__ float gelu_sig(float x) {
+    const float xc = __builtin_amdgcn_fmed3f(x, -8.0f, 8.0f);
+    const float x2 = xc * xc;
+    const float z = xc * fmaf(fmaf(-0.0009763994f, x2, 0.10652431f), x2, 2.3013635f);   // (a, b, c) * log2 e
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z));
+}
+
+
 // bijective XCD-aware block remap (8 XCDs, round-robin dispatch): blocks that
 // land on one XCD get a contiguous range of tile ids so they share L2 panels.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

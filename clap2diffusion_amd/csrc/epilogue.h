@@ -88,7 +88,7 @@ struct EpiPass {
 #pragma unroll
             for (int q = 0; q < W; q += 4) {
                 const float4 y = *reinterpret_cast<const float4*>(src + 16 + q);
-                v[q] *= gelu_f(y.x); v[q + 1] *= gelu_f(y.y); v[q + 2] *= gelu_f(y.z); v[q + 3] *= gelu_f(y.w);
+                v[q] *= gelu_sig(y.x); v[q + 1] *= gelu_sig(y.y); v[q + 2] *= gelu_sig(y.z); v[q + 3] *= gelu_sig(y.w);
             }
         } else if (p.act == C2D_ACT_GELU) {
 #pragma unroll
@@ -295,7 +295,7 @@ __device__ __forceinline__ void epi_rows_plain_t(const IgemmParams& p, const flo
                 }
             }
 #pragma unroll
-            for (int r = 0; r < W; ++r) v[r] *= gelu_f(g[r]);
+            for (int r = 0; r < W; ++r) v[r] *= gelu_sig(g[r]);
         } else if (p.act == C2D_ACT_GELU) {
 #pragma unroll
             for (int r = 0; r < W; ++r) v[r] = gelu_f(v[r]);

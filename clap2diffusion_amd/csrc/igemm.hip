@@ -234,7 +234,7 @@ __device__ __forceinline__ void epilogue_tiles(const IgemmParams& p, f32x4 (&acc
                 f16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float v = (h4[r] + hb[r]) * gelu_f(g4[r] + gb[r]);
+                    float v = (h4[r] + hb[r]) * gelu_sig(g4[r] + gb[r]);
                     if (p.resid) v += (float)rv[b][q][r];
                     o[r] = (f16)v;
                 }

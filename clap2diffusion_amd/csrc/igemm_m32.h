@@ -283,7 +283,7 @@ __device__ __forceinline__ void epilogue32_direct(const IgemmParams& p, const f3
                         gt[0] += bb.x; gt[1] += bb.y; gt[2] += bb.z; gt[3] += bb.w;
                     }
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] *= gelu_f(gt[r]);
+                    for (int r = 0; r < 4; ++r) v[r] *= gelu_sig(gt[r]);
                 }
                 if (trow) {
                     const h4 t = *reinterpret_cast<const h4*>(trow + j);

@@ -25,20 +25,6 @@
 
 namespace c2d {
 
-// GELU for the carried GEGLU epilogue: x * sigmoid(z), z = x' (a + b x'^2 + c x'^4), x' = x
-// clamped to [-8, 8] (z monotone there; sigmoid(z(+-8)) is 1 / 0 to 1e-12).  Coefficients fitted
-// (near-minimax) to the erf form 0.5 x (1 + erf(x / sqrt 2)) diffusers' GEGLU uses: max
-// |error| 3.4e-5 over the real line, below the fp16 rounding of every GEGLU output above
-// 0.07 in magnitude; 7 VALU + 2 transcendental issue slots against ~17 + 2 for the
-// Abramowitz-Stegun erf (gelu_f), the op count the carried epilogue hides under the MFMAs.
-// log2(e) is folded into the coefficients (exp2 on the hardware unit).
-__device__ __forceinline__ float gelu_sig(float x) {
-    const float xc = __builtin_amdgcn_fmed3f(x, -8.0f, 8.0f);
-    const float x2 = xc * xc;
-    const float z = xc * fmaf(fmaf(-0.0009763994f, x2, 0.10652431f), x2, 2.3013635f);   // (a, b, c) * log2 e
-    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z));
-}
-
 template <int NK, bool GG>
 __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
     constexpr int TN = 4, TMW = 6, BK = 64, NW = 8;
