@@ -733,7 +733,7 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 #define C2D_TILE_FN(ID) void run_tile_##ID(IgemmParams& p, int ksize, int cout, hipStream_t s)
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
-C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50);
+C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
 #if C2D_PART(1)
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
@@ -749,6 +749,8 @@ C2D_TILE_FN(7) { run_dma<2, 4, 4, 5, 2>(p, ksize, cout, s); }   // 128x320, 8 wa
 C2D_TILE_FN(1) { run_dma<4, 2, 4, 4, 3>(p, ksize, cout, s); }   // 256x128, 8 waves of 64x64
 C2D_TILE_FN(2) { run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s); }   // 128x128, 4 waves of 64x64
 C2D_TILE_FN(3) { run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s); }   // 64x64, 4 waves of 32x32
+C2D_TILE_FN(8) { run_dma<2, 2, 4, 5, 2>(p, ksize, cout, s); }   // 128x160, 4 waves of 64x80, 72 KiB: 2 per CU
+C2D_TILE_FN(9) { run_dma<2, 2, 2, 5, 2>(p, ksize, cout, s); }   // 64x160, 4 waves of 32x80, 56 KiB: 2 per CU
 #endif
 }  // namespace c2d
 #undef C2D_TILE_FN
@@ -773,6 +775,9 @@ static const DmaTile kDmaTiles[] = {
     {1, 256, 128, 1, 2.9f, true},
     {2, 128, 128, 1, 2.2f, true},
     {3, 64, 64, 3, 1.9f, true},
+    // two workgroups per CU (<= 80 KiB of LDS): the under-filled 1x1 / 3x3 shapes
+    {8, 128, 160, 2, 0.0f, false},
+    {9, 64, 160, 2, 0.0f, false},
 };
 struct DmaPlan { int id, split, nkt; };
 
@@ -844,10 +849,62 @@ static bool pps_eligible(const c2d_conv_desc* d) {
            ((uintptr_t)d->bias & 15) == 0 && (size_t)M * d->out_ld * 2 < (1u << 31);
 }
 
-static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok) {
+// Measured plans for the SD1.5 UNet shapes where the rules below lose >= 3 %: graph-replayed
+// forced-(tile, split) sweeps on MI355X at the three batches the configurations run
+// (scripts/sweep_tiles_graph.py; profiles/r03_sweep_b1.txt, r03_sweep_b4r96.txt,
+// r03_sweep_b8.txt).  The rules are tuned on N = 16 at 64^2; at N = 2 (c1 / c2) every shape is
+// latency bound, and at 96^2 (c5) the 256-row tile count is 288 = 1.1 rounds of 256 CUs.
+// Keyed on (ksize, M = N * H * W, kpad, cout, GEGLU); anything else goes through the rules.
+struct PlanHint { int ksize; long M; int kpad, cout; bool geglu; int id, split; };
+static const PlanHint kPlanHints[] = {
+    // N = 2, 64^2 (c1 / c2 latency)
+    {1, 8192, 1280, 320, false, 9, 1},        // ff2 L0: 18.5 -> 17.4 us
+    {1, 2048, 640, 1920, false, 9, 1},        // QKV L1: 13.7 -> 13.0
+    {1, 512, 1280, 1280, false, 3, 1},        // 1x1 L2: 14.0 -> 10.8
+    {1, 2048, 640, 5120, true, 41, 1},        // GEGLU L1: 32.7 -> 28.9
+    {3, 8192, 2880, 320, false, 7, 4},        // 3x3 L0 320: 49.3 -> 39.7
+    {3, 8192, 5760, 320, false, 40, 6},       // 3x3 L0 640 -> 320: 58.2 -> 54.7
+    {3, 8192, 8640, 320, false, 40, 8},       // 3x3 L0 960 -> 320: 72.8 -> 66.9
+    {3, 2048, 5760, 640, false, 7, 8},        // 3x3 L1 640: 42.3 -> 38.7
+    {3, 512, 11520, 1280, false, 8, 8},       // 3x3 L2 1280: 55.2 -> 49.7
+    {3, 512, 17280, 1280, false, 9, 8},       // 3x3 L2 1920 -> 1280: 75.2 -> 65.9
+    {3, 512, 23040, 1280, false, 7, 8},       // 3x3 L2 2560 -> 1280: 95.4 -> 80.3
+    // N = 8, 96^2 (c5)
+    {1, 73728, 320, 320, false, 7, 1},        // 1x1 L0: 53.9 -> 41.6
+    {1, 73728, 1280, 320, false, 7, 1},       // ff2 L0: 120.7 -> 104.6
+    {1, 18432, 640, 640, false, 41, 1},       // 1x1 L1: 38.2 -> 31.9
+    {1, 18432, 2560, 640, false, 41, 1},      // ff2 L1: 101.2 -> 74.6
+    {1, 4608, 5120, 1280, false, 40, 3},      // ff2 L2: 83.2 -> 79.2
+    {1, 4608, 1280, 10240, true, 41, 1},      // GEGLU L2: 153.8 -> 138.5
+    {1, 1152, 1280, 1280, false, 3, 1},       // 1x1 L3: 18.5 -> 15.6
+    {3, 18432, 5760, 640, false, 41, 1},      // 3x3 L1 640: 163.0 -> 147.7
+    {3, 1152, 11520, 1280, false, 41, 8},     // 3x3 L3 1280: 65.4 -> 61.2
+    {3, 1152, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 116.7 -> 96.1
+    // N = 16, 64^2 (c3)
+    {1, 4096, 1280, 1280, false, 8, 1},       // 1x1 L2: 27.2 -> 24.5
+    {1, 1024, 1280, 1280, false, 3, 1},       // 1x1 mid: 18.9 -> 13.5
+    {3, 1024, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 97.2 -> 91.3
+};
+
+static bool plan_hint(int ksize, long M, int kpad, int cout, bool geglu, DmaPlan& pl) {
+    for (const PlanHint& h : kPlanHints)
+        if (h.ksize == ksize && h.M == M && h.kpad == kpad && h.cout == cout && h.geglu == geglu) {
+            const int nk = kpad / 64;
+            const int nkt = (nk + h.split - 1) / h.split;
+            pl = {h.id, (nk + nkt - 1) / nkt, nkt};
+            return true;
+        }
+    return false;
+}
+
+static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize) {
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
     int id = gemm_tile();
+    if (!id) {
+        DmaPlan pl;
+        if (plan_hint(ksize, M, kpad, cout, geglu, pl)) return pl;
+    }
     if (id == 7 && geglu) id = 0;
     if (id == 50) {
         if (pps_ok) return {50, 1, nk};
@@ -923,6 +980,8 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 7: return run_tile_7(p, ksize, cout, s);
         case 1: return run_tile_1(p, ksize, cout, s);
         case 2: return run_tile_2(p, ksize, cout, s);
+        case 8: return run_tile_8(p, ksize, cout, s);
+        case 9: return run_tile_9(p, ksize, cout, s);
         default: return run_tile_3(p, ksize, cout, s);
     }
 }
@@ -941,7 +1000,7 @@ extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
     if (!dma_eligible(d)) return 0;
     const long M = (long)d->n * d->oh * d->ow;
-    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d));
+    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize);
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
 
@@ -954,7 +1013,7 @@ extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* 
         return C2D_OK;
     }
     const long M = (long)d->n * d->oh * d->ow;
-    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d));
+    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize);
     if (pl.split > 1) {
         const size_t need = (size_t)pl.split * M * d->cout * sizeof(float);
         if (!(d->ws && d->ws_bytes >= need && aligned16(d->ws))) pl.split = 1;
@@ -1020,7 +1079,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d));
+        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize);
         if (pl.split > 1) {
             const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
             if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {

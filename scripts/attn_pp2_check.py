@@ -1,0 +1,75 @@
+"""d = 40 self-attention: correctness vs fp32 SDPA and graph-replayed timing of whichever kernel
+the library's C2D_ATTN_PP2 setting selects (run once per setting, same box).
+python scripts/attn_pp2_check.py"""
+import os
+import sys
+from pathlib import Path
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from clap2diffusion_amd import ops  # noqa: E402
+
+dev = torch.device("cuda")
+SHAPES = [  # name, batch, heads, lq, lk
+    ("L0 self N=16 4096", 16, 8, 4096, 4096),
+    ("L0 self N=8 4096 (CFG prefix)", 8, 8, 4096, 4096),
+    ("c5 self N=8 9216", 8, 8, 9216, 9216),
+    ("N=2 4096 (c2)", 2, 8, 4096, 4096),
+    ("odd 300x256", 3, 8, 300, 256),
+]
+tag = os.environ.get("C2D_ATTN_PP2", "0")
+
+
+def graph_ms(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) / iters)
+    return best
+
+
+for name, b, h, lq, lk in SHAPES:
+    d = 40
+    gen = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn(b * lq, h * d, device=dev, generator=gen).half()
+    k = torch.randn(b * lk, h * d, device=dev, generator=gen).half()
+    v = torch.randn(b * lk, h * d, device=dev, generator=gen).half()
+    # spikes force the running-max rescale mid-sequence: one key row of image 0 aligned with
+    # the first query row (keys past the first tiles)
+    k.view(b, lk, h, d)[0, lk // 2 + 5] = q.view(b, lq, h, d)[0, 0] * 4
+    k.view(b, lk, h, d)[1 % b, lk - 3] = q.view(b, lq, h, d)[1 % b, 7] * 3
+    o = torch.empty_like(q)
+    call = lambda: ops.attention(q, k, v, b, h, lq, lk, d, out=o)  # noqa: E731
+    ms = graph_ms(call)
+    call()
+    torch.cuda.synchronize()
+    nb = min(b, 2)
+    qh = q.view(b, lq, h, d).transpose(1, 2)[:nb].float()
+    kh = k.view(b, lk, h, d).transpose(1, 2)[:nb].float()
+    vh = v.view(b, lk, h, d).transpose(1, 2)[:nb].float()
+    ref = F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(nb, lq, h * d)
+    got = o.view(b, lq, h * d)[:nb].float()
+    err = ((got - ref).norm() / ref.norm()).item()
+    emax = ((got - ref).abs().max() / ref.abs().max()).item()
+    fl = 4.0 * b * h * lq * lk * d
+    print(f"PP2={tag} {name:30s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  rel-L2 {err:.2e} rel-max {emax:.2e}",
+          flush=True)
