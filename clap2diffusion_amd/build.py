@@ -59,19 +59,22 @@ def _compile(unit, build_dir: Path, defines=()) -> Path:
     return obj
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bool = False) -> Path:
+def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bool = False,
+          variant: str = "", variant_defines: tuple = ()) -> Path:
     """ablation=True builds libc2d_hip_abl.so with -DC2D_ENABLE_ABLATION (timing-ablation
     switches live; wrong results by design) for scripts/gpu_gemm_abl.sh via C2D_LIB; the
-    production libc2d_hip.so never contains them."""
-    defines = ("C2D_ENABLE_ABLATION",) if ablation else ()
-    lib_path = PKG / ("libc2d_hip_abl.so" if ablation else "libc2d_hip.so")
-    stamp = PKG / (".libc2d_hip_abl.stamp" if ablation else ".libc2d_hip.stamp")
+    production libc2d_hip.so never contains them.  variant="x" with variant_defines builds
+    libc2d_hip_x.so (compile-time A/B candidates, loaded through C2D_LIB)."""
+    defines = ("C2D_ENABLE_ABLATION",) if ablation else tuple(variant_defines)
+    stem = "libc2d_hip_abl" if ablation else (f"libc2d_hip_{variant}" if variant else "libc2d_hip")
+    lib_path = PKG / f"{stem}.so"
+    stamp = PKG / f".{stem}.stamp"
     dig = _digest(defines)
     if lib_path.exists() and stamp.exists() and stamp.read_text().strip() == dig and not force:
         if verbose:
             print(f"[c2d] {lib_path.name} up to date ({dig})")
         return lib_path
-    build_dir = ROOT / "build" / ("c2d_abl" if ablation else "c2d")
+    build_dir = ROOT / "build" / ("c2d_abl" if ablation else (f"c2d_{variant}" if variant else "c2d"))
     build_dir.mkdir(parents=True, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda u: _compile(u, build_dir, defines), UNITS))
@@ -99,6 +102,8 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=4)
     ap.add_argument("--ablation", action="store_true", help="build libc2d_hip_abl.so (timing ablations)")
+    ap.add_argument("--variant", default="", help="build libc2d_hip_<variant>.so with --define D ...")
+    ap.add_argument("--define", action="append", default=[])
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs, ablation=a.ablation)
+    build(force=a.force, jobs=a.jobs, ablation=a.ablation, variant=a.variant, variant_defines=tuple(a.define))
     sys.exit(0)

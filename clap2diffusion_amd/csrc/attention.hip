@@ -19,6 +19,9 @@ namespace c2d {
 #ifndef ATTN_WPE
 #define ATTN_WPE 4
 #endif
+#ifndef C2D_ATTN_YPRIO
+#define C2D_ATTN_YPRIO 0
+#endif
 
 template <int D> struct AttnCfg {
     // K dim of QK^T: full 32-deep chunks on 16x16x32 MFMAs plus, when the rest is
@@ -237,6 +240,9 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     float m_run[2] = {NEGC ? 0.f : -1e30f, NEGC ? 0.f : -1e30f}, l_run[2] = {0.f, 0.f};
     f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
+    // static priority for the second-dispatched half of an 8-wave block (cdna_hip_programming.md
+    // T5 static form: waves 4-7 otherwise lose VALU arbitration to the older half)
+    if (C2D_ATTN_YPRIO && NWV == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < ntiles; ++t) {
         if (!RES && t + 1 < ntiles && !C2D_ABL(abl, 1)) gload(t + 1);
         const char* Kt = Ks + (RES ? t * SLOT : 0);
@@ -712,242 +718,6 @@ __global__ void __launch_bounds__(256) attn_pp_kernel(const f16* __restrict__ q,
 #undef KB
 #undef VB
 
-// ---------------------------------------------------------------------------
-// Two-group ping-pong for the d = 40 self-attention (the level-0 4096-key and c5's 9216-key
-// shapes; keys a multiple of 64, no mask / bias).  The one-group kernel is VALU-issue bound
-// (PMC: VALU issue 0.64, MFMA busy 0.47): every wave of a block runs QK^T -> softmax -> PV in
-// the same order between the same barriers, so on a SIMD the matrix pipe idles while its
-// waves exponentiate and the VALU idles while they multiply.  Here the 8 waves of the block
-// form two groups of 4 (one wave of each per SIMD: waves are dealt to SIMDs round robin)
-// that run the same phase sequence one barrier apart:
-//   M_t (matrix): stage half of K/V tile t+1 into LDS, issue the global loads of tile t+2,
-//                 S(t) = K(t) Q^T [+ C = -m]  and  O^T += V(t-1) P(t-1)^T        (MFMA)
-//   V_t (vector): online softmax of S(t): lane max, lazy 2^8 rescale of O, exp2 -> P(t)
-// so while one group's waves exponentiate, the other's issue MFMAs on the same SIMD.  Each
-// wave owns QW = 16 QG queries; fragment layouts, the K swizzle, the V^T transposed reads,
-// the ones column that carries the row sum through the PV MFMA and the NEGC form (Q pre-
-// scaled by scale * log2 e, the running max folded into the MFMA's C) are those of
-// attn_fwd_kernel.
-// K/V ring: 3 slots.  Tile t is read as K in M_t (group 0 at barrier interval 2t, group 1 at
-// 2t + 1) and as V in M_{t+1} (2t + 2, 2t + 3); each group writes its 32-row half of tile t+1
-// into slot (t+1) % 3 in its M_t (group 0 at 2t, group 1 at 2t + 1) -- that slot last held
-// tile t-2, whose V reads ended at interval 2t - 1 -- and waits for its LDS writes
-// (lgkmcnt(0)) before the barrier that ends the interval, so tile t+1 is complete before
-// either group's M_{t+1}.  The global loads of a tile are issued two intervals before their
-// LDS writes.
-template <int D, int QG>
-__global__ void __launch_bounds__(512) attn_pp2_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
-                                                       int ldk, const f16* __restrict__ v, int ldv, f16* __restrict__ o,
-                                                       int ldo, int heads, int lq, int lk, float scale_log2,
-                                                       int kv_div, int nqb) {
-    using C = AttnCfg<D>;
-    static_assert(C::KSW && C::SUM_MFMA && C::NDC_FULL == 2 && !C::TAIL, "ping-pong attention: d = 40 layout only");
-    constexpr int NS = 3, SLOT = C::K_BYTES + C::V_BYTES;
-    constexpr int QW = 16 * QG;                 // queries per wave
-    constexpr int NCP = 32 * C::DCH * 2;        // 16-B copies of a group's half tile (K and V rows)
-    constexpr int NCT = (NCP + 255) / 256;      // per thread
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int gr = wave >> 2, gt = tid & 255;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int bh = tile / nqb, qb = tile - bh * nqb;
-    const int b = bh / heads, h = bh - b * heads;
-    const int bk = b / kv_div;
-    const int q0 = qb * (8 * QW) + wave * QW;
-    const int g = lane >> 4, li = lane & 15;
-
-    // pads of every slot: K chunks >= DCH zero; V pad columns zero except the ones column at D
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-        for (int idx = tid; idx < 64 * (C::DP / 8 - C::DCH); idx += 512) {
-            const int row = idx / (C::DP / 8 - C::DCH), ch = C::DCH + idx % (C::DP / 8 - C::DCH);
-            *reinterpret_cast<f16x8*>(smem + sl * SLOT + k_off<D>(row, ch)) = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
-        }
-        for (int idx = tid; idx < 64 * (C::DV / 8 - C::DCH); idx += 512) {
-            const int row = idx / (C::DV / 8 - C::DCH), ch = C::DCH + idx % (C::DV / 8 - C::DCH);
-            f16x8 z = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
-            if (ch == C::DCH) z[0] = (f16)1.0f;
-            *reinterpret_cast<f16x8*>(smem + sl * SLOT + C::K_BYTES + row * C::VS + ch * 16) = z;
-        }
-    }
-
-    // Q fragments (B operand of S^T = K Q^T), pre-scaled by scale * log2 e
-    f16x8 qf[QG][2];
-#pragma unroll
-    for (int qg = 0; qg < QG; ++qg) {
-        const int qi = q0 + qg * 16 + li;
-#pragma unroll
-        for (int dc = 0; dc < 2; ++dc) {
-            const int d0 = dc * 32 + g * 8;
-            f16x8 x = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
-            if (qi < lq && d0 < D) x = *reinterpret_cast<const f16x8*>(q + ((size_t)b * lq + qi) * ldq + h * D + d0);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = (f16)((float)x[j] * scale_log2);
-            qf[qg][dc] = x;
-        }
-    }
-
-    // staging of this group's half tile: copy c < NCP -> (K | V, row 32 gr + r, chunk ch)
-    const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
-    const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
-    f16x8 rg[NCT];
-    auto gload = [&](int t) {
-#pragma unroll
-        for (int i = 0; i < NCT; ++i) {
-            const int c = gt + 256 * i;
-            if (256 * i + 255 < NCP || c < NCP) {
-                const int isv = c >= 32 * C::DCH, cc = isv ? c - 32 * C::DCH : c;
-                const int row = 32 * gr + cc / C::DCH, ch = cc - (cc / C::DCH) * C::DCH;
-                const size_t key = (size_t)t * 64 + row;
-                rg[i] = isv ? *reinterpret_cast<const f16x8*>(vbase + key * ldv + ch * 8)
-                            : *reinterpret_cast<const f16x8*>(kbase + key * ldk + ch * 8);
-            }
-        }
-    };
-    auto swrite = [&](int sl) {
-#pragma unroll
-        for (int i = 0; i < NCT; ++i) {
-            const int c = gt + 256 * i;
-            if (256 * i + 255 < NCP || c < NCP) {
-                const int isv = c >= 32 * C::DCH, cc = isv ? c - 32 * C::DCH : c;
-                const int row = 32 * gr + cc / C::DCH, ch = cc - (cc / C::DCH) * C::DCH;
-                char* dst = smem + sl * SLOT + (isv ? C::K_BYTES + row * C::VS + ch * 16 : k_off<D>(row, ch));
-                *reinterpret_cast<f16x8*>(dst) = rg[i];
-            }
-        }
-    };
-
-    f32x4 acc[C::NDT][QG];
-#pragma unroll
-    for (int dt = 0; dt < C::NDT; ++dt)
-#pragma unroll
-        for (int qg = 0; qg < QG; ++qg) acc[dt][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float m_run[QG];
-    f32x4 negm[QG];
-#pragma unroll
-    for (int qg = 0; qg < QG; ++qg) {
-        m_run[qg] = 0.f;
-        negm[qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    f32x4 s[QG][4];
-    f16x8 pf[QG][2];
-
-    // sched_barrier(0) on both sides: nothing of one phase migrates into the next
-#define C2D_BAR()                                   \
-    do {                                            \
-        __builtin_amdgcn_sched_barrier(0);          \
-        asm volatile("" ::: "memory");              \
-        __builtin_amdgcn_s_barrier();               \
-        asm volatile("" ::: "memory");              \
-        __builtin_amdgcn_sched_barrier(0);          \
-    } while (0)
-    const int ntiles = lk / 64;
-    gload(0);
-    __syncthreads();   // pad zeroing done before the first tile lands
-    swrite(0);
-    if (ntiles > 1) gload(1);
-    __syncthreads();   // tile 0 complete
-    if (gr) C2D_BAR();   // group 1 runs one barrier behind group 0
-
-    for (int t = 0; t <= ntiles; ++t) {
-        // ---- M_t: stage tile t+1 (this group's half), loads of tile t+2, QK^T(t), PV(t-1)
-        if (t + 1 < ntiles) {
-            swrite((t + 1) % NS);
-            if (t + 2 < ntiles) gload(t + 2);
-        }
-        __builtin_amdgcn_s_setprio(1);
-        if (t < ntiles) {
-            const char* Kt = smem + (t % NS) * SLOT;
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg) {
-#pragma unroll
-                for (int dc = 0; dc < 2; ++dc) {
-                    const f16x8 kf = *reinterpret_cast<const f16x8*>(Kt + k_off<D>(kg * 16 + li, dc * 4 + g));
-#pragma unroll
-                    for (int qg = 0; qg < QG; ++qg)
-                        s[qg][kg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf[qg][dc], dc == 0 ? negm[qg] : s[qg][kg],
-                                                                            0, 0, 0);
-                }
-            }
-        }
-        if (t > 0) {
-            const char* Vt = smem + ((t - 1) % NS) * SLOT + C::K_BYTES;
-#pragma unroll
-            for (int dt = 0; dt < C::NDT; ++dt) {
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb) {
-                    const int qq = li >> 2, pp = li & 3;
-                    const int row1 = kb * 32 + g * 4 + qq;
-                    const char* a1 = Vt + row1 * C::VS + (dt * 16 + pp * 4) * 2;
-                    const char* a2 = a1 + 16 * C::VS;
-                    s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a1);
-                    s16x4 t2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(LDS_AS char*)a2);
-                    f16x8 vf;
-                    f16x4 h1 = __builtin_bit_cast(f16x4, t1), h2 = __builtin_bit_cast(f16x4, t2);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) { vf[j] = h1[j]; vf[4 + j] = h2[j]; }
-#pragma unroll
-                    for (int qg = 0; qg < QG; ++qg)
-                        acc[dt][qg] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf[qg][kb], acc[dt][qg], 0, 0, 0);
-                }
-            }
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0): staged half + reads done
-        C2D_BAR();
-        // ---- V_t: online softmax of S(t) (log2 domain, lazy 2^8 rescale) -> P(t)
-        if (t < ntiles) {
-#pragma unroll
-            for (int qg = 0; qg < QG; ++qg) {
-                const float lmx = lane_max16(s[qg]);
-                if (t == 0 || __builtin_amdgcn_ballot_w64(lmx > 8.0f)) {
-                    const float mx = quad_max(lmx);
-                    const float delta = t == 0 ? mx : fmaxf(mx, 0.f);
-                    const float alpha = __builtin_amdgcn_exp2f(-delta);
-                    m_run[qg] += delta;
-                    negm[qg] = (f32x4){-m_run[qg], -m_run[qg], -m_run[qg], -m_run[qg]};
-#pragma unroll
-                    for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
-#pragma unroll
-                    for (int kg = 0; kg < 4; ++kg) s[qg][kg] -= delta;
-                }
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        pf[qg][kb][j] = (f16)__builtin_amdgcn_exp2f(s[qg][2 * kb][j]);
-                        pf[qg][kb][4 + j] = (f16)__builtin_amdgcn_exp2f(s[qg][2 * kb + 1][j]);
-                    }
-            }
-        }
-        C2D_BAR();
-    }
-    if (!gr) C2D_BAR();   // balance the stagger
-#undef C2D_BAR
-
-    // epilogue: lane holds O[query li][d = 16 dt + 4 g + r]; row sum in the ones column D
-#pragma unroll
-    for (int qg = 0; qg < QG; ++qg) {
-        const float l = __shfl(acc[D / 16][qg][D % 4], li + 16 * ((D % 16) / 4));
-        const float inv = 1.0f / l;
-        const int qi = q0 + qg * 16 + li;
-        if (qi >= lq) continue;
-        f16* orow = o + ((size_t)b * lq + qi) * ldo + h * D;
-#pragma unroll
-        for (int dt = 0; dt < C::NDT; ++dt) {
-            const int d0 = dt * 16 + g * 4;
-            if (d0 < D) {
-                f16x4 ov;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) ov[r] = (f16)(acc[dt][qg][r] * inv);
-                *reinterpret_cast<f16x4*>(orow + d0) = ov;
-            }
-        }
-    }
-}
-
 // C2D_ATTN_PP=1 selects the double-buffered, software-pipelined d=40 kernel.  Measured
 // slower than the single-buffered one on MI355X (L0 self 4096x4096: 779 vs 653 us): the
 // in-flight S tile takes it to 148 VGPR + 24 AGPR = 2 waves/SIMD vs 126 + 40 = 3 for
@@ -962,7 +732,6 @@ static bool attn_negc() { return tuning().attn_negc != 0; }
 static bool attn_res() { return tuning().attn_res != 0; }
 static bool attn_w8() { return tuning().attn_w8 != 0; }
 static int attn_pipelined() { return tuning().attn_pp; }
-static int attn_pingpong() { return tuning().attn_pp2; }
 
 // attention with an additive per-key bias: the fma-softmax kernels (resident K/V for
 // lk <= 128, streaming otherwise); the bias is pre-multiplied by 1 / scale
@@ -1034,23 +803,6 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
                        ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb, \
                        attn_abl())
     if constexpr (D == 40) {
-        // two-group ping-pong (attn_pp2_kernel): C2D_ATTN_PP2 = queries per wave / 16 (2 or 4), 0 = off
-        const int pp2 = attn_pingpong();
-        if (lk % 64 == 0 && lk >= 256 && (pp2 == 2 || pp2 == 4)) {
-            const int qblk = pp2 * 16 * 8;
-            const int nq = (lq + qblk - 1) / qblk;
-            dim3 g2((unsigned)(nq * batch * heads));
-            constexpr int smem2 = 3 * (C::K_BYTES + C::V_BYTES);
-            if (pp2 == 2)
-                hipLaunchKernelGGL((attn_pp2_kernel<D, 2>), g2, dim3(512), smem2, s, (const f16*)q, ldq, (const f16*)k,
-                                   ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f,
-                                   kv_div, nq);
-            else
-                hipLaunchKernelGGL((attn_pp2_kernel<D, 4>), g2, dim3(512), smem2, s, (const f16*)q, ldq, (const f16*)k,
-                                   ldk, (const f16*)v, ldv, (f16*)o, ldo, heads, lq, lk, scale * 1.4426950408889634f,
-                                   kv_div, nq);
-            return check_launch();
-        }
         // 8-wave blocks (256 queries): one K / V staging chunk per thread instead of two
         // (L0: 586-628 -> 560-594 us, same box); d = 80 measured 72 -> 76 us with them
         if (lk % 64 == 0 && lk >= 256 && attn_negc() && attn_w8()) {

@@ -32,7 +32,6 @@ const Tuning& tuning() {
         t.attn_res = env_int("C2D_ATTN_RES", 1);
         t.attn_w8 = env_int("C2D_ATTN_W8", 1);
         t.attn_pp = env_int("C2D_ATTN_PP", 0);
-        t.attn_pp2 = env_int("C2D_ATTN_PP2", 0);          // d = 40 two-group ping-pong: 2 / 4 queries-per-wave / 16
         t.gn_blocks = env_int("C2D_GN_BLOCKS", 512);
         if (t.gn_blocks < 64) t.gn_blocks = 512;
         t.gn_apply_blocks = env_int("C2D_GN_APPLY_BLOCKS", 2048);

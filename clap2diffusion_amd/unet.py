@@ -138,16 +138,22 @@ class BasicTransformerBlock(nn.Module):
         return ops.add(out.to(h.dtype).contiguous(), h)
 
     def forward(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict,
-                encoder_attention_mask: torch.Tensor | None = None, cfg_dup: bool = False) -> torch.Tensor:
+                encoder_attention_mask: torch.Tensor | None = None,
+                cfg_dup: torch.Tensor | None = None) -> torch.Tensor:
         """h: [B, L, C] fp16 (updated in place by the fused residual epilogues).
         encoder_attention_mask: additive key bias for attn2 (diffusers BasicTransformerBlock).
-        cfg_dup: h holds one half of a CFG pair whose halves are identical up to here; the
-        self-attention runs on it once and the result is duplicated before attn2, the first
-        op where the [uncond, cond] halves differ (UNet2DConditionModel.forward_nhwc)."""
+        cfg_dup: h holds one half of a CFG pair whose halves are identical up to here, and is the
+        first half of this [2B, L, C] buffer; the self-attention runs on it once and its output
+        is copied into the second half before attn2, the first op where the [uncond, cond] halves
+        differ (UNet2DConditionModel.forward_nhwc)."""
         kw = cross_attention_kwargs or {}
         h = self._attend(self.attn1, self.norm1(h), h, None, None, kw)
-        if cfg_dup:
-            h = torch.cat([h, h], 0)
+        if cfg_dup is not None:
+            n = h.shape[0]
+            if h.data_ptr() != cfg_dup.data_ptr():   # a plugin processor returned a new tensor
+                cfg_dup[:n].copy_(h)
+            cfg_dup[n:].copy_(cfg_dup[:n])
+            h = cfg_dup
         h = self._attend(self.attn2, self.norm2(h), h, ehs, encoder_attention_mask, kw)
         b, l, c = h.shape
         h2 = h.view(b * l, c)
@@ -164,16 +170,25 @@ class Transformer2DModel(nn.Module):
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(c, heads, cross_dim)])
         self.proj_out = HConv2d(c, c, 1)
 
-    def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None, cfg_dup: bool = False):
-        """cfg_dup: x is one half of a CFG pair with identical halves; the output is the full
-        pair (the block duplicates its state before the cross-attention)."""
+    def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None,
+                cfg_dup: torch.Tensor | None = None):
+        """cfg_dup: x is one half of a CFG pair with identical halves and the first half of this
+        [2N, H, W, C] buffer; the output is the full pair (the block duplicates its state before
+        the cross-attention, and x into the buffer's second half for proj_out's residual).  The
+        duplicates are one device copy of a half each -- a torch.cat of the halves read 1 and
+        wrote 2 half-tensors (30 us per call at level 0)."""
         n, hh, ww, c = x.shape
-        h = self.proj_in(self.norm.apply(x))
+        if cfg_dup is None:
+            h = self.proj_in(self.norm.apply(x))
+            t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs,
+                                           encoder_attention_mask)
+            return self.proj_out(t.view(n, hh, ww, c), resid=x)
+        hb = x.new_empty((2 * n, hh * ww, c))
+        h = self.proj_in(self.norm.apply(x), out=hb[:n].view(n, hh, ww, c))
         t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
-                                       cfg_dup=cfg_dup)
-        if cfg_dup:
-            x, n = torch.cat([x, x], 0), 2 * n
-        return self.proj_out(t.view(n, hh, ww, c), resid=x)
+                                       cfg_dup=hb)
+        cfg_dup[n:].copy_(cfg_dup[:n])
+        return self.proj_out(t.view(2 * n, hh, ww, c), resid=cfg_dup)
 
 
 class ResnetBlock2D(nn.Module):
@@ -189,13 +204,13 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = HConv2d(cin, cout, 1) if cin != cout else None
         self.temb_off = None  # column offset into the batched time_emb_proj output
 
-    def forward(self, x, temb_all=None, skip=None):
+    def forward(self, x, temb_all=None, skip=None, out=None):
         temb = None
         if temb_all is not None:
             temb = temb_all[:, self.temb_off:self.temb_off + self.cout]
         h = self.conv1(self.norm1.apply(x, skip, silu=True), temb=temb)
         res = self.conv_shortcut(x, x2=skip) if self.conv_shortcut is not None else x
-        return self.conv2(self.norm2.apply(h, silu=True), resid=res)
+        return self.conv2(self.norm2.apply(h, silu=True), resid=res, out=out)
 
 
 class Downsample2D(nn.Module):
@@ -380,16 +395,28 @@ class UNet2DConditionModel(nn.Module):
         shared = cfg_pair and self.cfg_shared_prefix_ok()
         if cfg_pair and not shared:
             x = torch.cat([x, x], 0)
-        h = self.conv_in(x)
-        skips = [torch.cat([h, h], 0) if shared else h]
+        if shared:   # conv_in runs on one half, written into the first half of the skip buffer
+            n0 = x.shape[0]
+            skip0 = x.new_empty((2 * n0, x.shape[1], x.shape[2], self.conv_in.cout))
+            h = self.conv_in(x, out=skip0[:n0])
+            skip0[n0:].copy_(skip0[:n0])
+            skips = [skip0]
+        else:
+            h = self.conv_in(x)
+            skips = [h]
         for i, blk in enumerate(self.down_blocks):
             for j, r in enumerate(blk.resnets):
                 pre = shared and i == 0 and j == 0   # still on one half of the CFG pair
-                h = r(h, temb_all)
+                if pre:   # the resnet output lands in the first half of its CFG-pair buffer
+                    hb = h.new_empty((2 * h.shape[0], h.shape[1], h.shape[2], r.cout))
+                    h = r(h, temb_all, out=hb[:h.shape[0]])
+                else:
+                    h = r(h, temb_all)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw, em, cfg_dup=pre)
+                    h = blk.attentions[j](h, ehs, kw, em, cfg_dup=hb if pre else None)
                 elif pre:
-                    h = torch.cat([h, h], 0)
+                    hb[h.shape[0]:].copy_(h)
+                    h = hb
                 skips.append(h)
             if hasattr(blk, "downsamplers"):
                 h = blk.downsamplers[0](h)

@@ -1,6 +1,6 @@
 """d = 40 self-attention: correctness vs fp32 SDPA and graph-replayed timing of whichever kernel
-the library's C2D_ATTN_PP2 setting selects (run once per setting, same box).
-python scripts/attn_pp2_check.py"""
+the library selects (TAG labels the run).
+python scripts/attn_d40_check.py"""
 import os
 import sys
 from pathlib import Path
@@ -19,7 +19,7 @@ SHAPES = [  # name, batch, heads, lq, lk
     ("N=2 4096 (c2)", 2, 8, 4096, 4096),
     ("odd 300x256", 3, 8, 300, 256),
 ]
-tag = os.environ.get("C2D_ATTN_PP2", "0")
+tag = os.environ.get("TAG", "")
 
 
 def graph_ms(fn, iters=10):
@@ -71,5 +71,5 @@ for name, b, h, lq, lk in SHAPES:
     err = ((got - ref).norm() / ref.norm()).item()
     emax = ((got - ref).abs().max() / ref.abs().max()).item()
     fl = 4.0 * b * h * lq * lk * d
-    print(f"PP2={tag} {name:30s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  rel-L2 {err:.2e} rel-max {emax:.2e}",
+    print(f"{tag} {name:30s} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TF/s  rel-L2 {err:.2e} rel-max {emax:.2e}",
           flush=True)

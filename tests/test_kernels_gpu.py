@@ -144,7 +144,7 @@ def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
 
 # every tile configuration left in igemm.hip's kDmaTiles, forced through
 # c2d_set_plan_override and confirmed through c2d_conv2d_igemm_plan
-DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3]
+DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3, 8, 9]
 
 
 @pytest.mark.parametrize("tile", DMA_TILE_IDS)
@@ -228,7 +228,7 @@ def test_epilogue_operand_forms(dev, force_plan, tile, cout, temb, resid, bias):
     close(nchw(out), ref)
 
 
-@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 40)])   # odd column tiles: no GEGLU
+@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 8, 9, 40)])   # odd column tiles: no GEGLU
 def test_every_dma_tile_forced_geglu(dev, force_plan, tile):
     m, cin, inner = 1024, 320, 640
     force_plan(tile, 1)

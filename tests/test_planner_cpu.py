@@ -1,0 +1,45 @@
+"""The implicit-GEMM planner (c2d_conv2d_igemm_plan: host code, no GPU needed): the measured
+plan table for the SD1.5 UNet shapes at the c2 / c3 / c5 batches (igemm.hip kPlanHints,
+profiles/r03_sweep_*.txt) routes those shapes, and a shape the table does not hold falls
+through to the rules."""
+import ctypes
+
+import pytest
+
+
+def _plan(cin, cout, n, h, k, ws=True, geglu=False):
+    import torch  # noqa: F401  (binds the library to torch's HIP runtime first)
+    from clap2diffusion_amd import _lib, ops
+    L = _lib.lib()
+    d = _lib.ConvDesc()
+    d.c0, d.c1, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, 0, n, h, h, h, h, k, 1
+    d.cout, d.kpad = cout, ops.kpad_of(k * k * cin)
+    if geglu:
+        d.act = 1   # C2D_ACT_GEGLU
+    if ws:   # a workspace large enough for any split (the planner only reads the pointer / size)
+        d.ws, d.ws_bytes = 16, 1 << 40
+    tile, split = ctypes.c_int(-1), ctypes.c_int(-1)
+    assert L.c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tile), ctypes.byref(split)) == 0
+    return tile.value, split.value
+
+
+@pytest.mark.parametrize("cin,cout,n,h,k,geglu,want", [
+    (320, 320, 2, 64, 3, False, (7, 4)),        # c2: L0 resnet conv
+    (640, 640, 2, 32, 3, False, (7, 8)),        # c2: L1 resnet conv
+    (2560, 1280, 2, 16, 3, False, (7, 8)),      # c2: L2 up-block conv
+    (1280, 1280, 2, 16, 1, False, (3, 1)),      # c2: L2 projections
+    (640, 5120, 2, 32, 1, True, (41, 1)),       # c2: L1 GEGLU
+    (320, 320, 8, 96, 1, False, (7, 1)),        # c5: L0 projections
+    (640, 640, 8, 48, 3, False, (41, 1)),       # c5: L1 resnet conv
+    (1280, 1280, 16, 16, 1, False, (8, 1)),     # c3: L2 projections (128 x 160, two per CU)
+    (1280, 1280, 16, 8, 1, False, (3, 1)),      # c3: mid-block projections
+])
+def test_plan_table_routes_unet_shapes(cin, cout, n, h, k, geglu, want):
+    assert _plan(cin, cout, n, h, k, geglu=geglu) == want
+
+
+def test_table_split_needs_workspace_and_other_shapes_use_the_rules():
+    # without a workspace a split-K table entry keeps its tile and runs one K slice
+    assert _plan(320, 320, 2, 64, 3, ws=False) == (7, 1)
+    # c3's level-0 resnet conv is not in the table: the rules' 256 x 320 ping-pong tile
+    assert _plan(320, 320, 16, 64, 3) == (40, 1)
