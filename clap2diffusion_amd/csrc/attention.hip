@@ -19,9 +19,6 @@ namespace c2d {
 #ifndef ATTN_WPE
 #define ATTN_WPE 4
 #endif
-#ifndef C2D_ATTN_YPRIO
-#define C2D_ATTN_YPRIO 0
-#endif
 
 template <int D> struct AttnCfg {
     // K dim of QK^T: full 32-deep chunks on 16x16x32 MFMAs plus, when the rest is
@@ -240,9 +237,6 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     float m_run[2] = {NEGC ? 0.f : -1e30f, NEGC ? 0.f : -1e30f}, l_run[2] = {0.f, 0.f};
     f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
-    // static priority for the second-dispatched half of an 8-wave block (cdna_hip_programming.md
-    // T5 static form: waves 4-7 otherwise lose VALU arbitration to the older half)
-    if (C2D_ATTN_YPRIO && NWV == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
     for (int t = 0; t < ntiles; ++t) {
         if (!RES && t + 1 < ntiles && !C2D_ABL(abl, 1)) gload(t + 1);
         const char* Kt = Ks + (RES ? t * SLOT : 0);
