@@ -27,6 +27,9 @@
 // DVFS item 7: ~1.12-1.15x the FLOP/s on random data).
 #pragma once
 
+#ifndef C2D_PP16_PH
+#define C2D_PP16_PH 4
+#endif
 #ifndef C2D_PP16_LGKM_ALL
 #define C2D_PP16_LGKM_ALL 1   // 0: lgkmcnt(0) only in phase 3 (measured neutral: bench 7.845 / 7.840 vs 7.850 / 7.837)
 #endif
@@ -46,7 +49,12 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
     typedef M32Loader<BM, BN, BK, NW, KS> Loader;
     constexpr int P = Loader::PMAX;
     static_assert(Loader::PMIN == P, "every wave deals the same pieces");
-    constexpr int PPH = (P + 2) / 3;   // pieces per phase, phases 0..2
+    // phases per K step: 4 = (k32 half, row half), 20-MFMA sections; 2 = k32 half, 40-MFMA
+    // sections (half the barriers; all eight A row tiles' fragments live; every DMA piece of
+    // the next K step dealt in phase 0, so phase 1 is its landing time)
+    constexpr int PH = C2D_PP16_PH, RT = PH == 4 ? 4 : 8;
+    static_assert(PH == 2 || PH == 4, "pp16 phases per K step");
+    constexpr int PPH = (P + PH - 2) / (PH - 1);   // pieces per phase, phases 0..PH-2
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -77,15 +85,15 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
     C2D_BAR();
     if (wr) C2D_BAR();   // group 1 runs one barrier behind group 0
 
-    f16x8 fa[4], fb[TN];
+    f16x8 fa[RT], fb[TN];
     for (int kt = kb; kt < ke; ++kt) {
         const char* S = smem + (kt & 1) * STAGE;
         char* Wn = smem + ((kt + 1) & 1) * STAGE;
         const bool nxt = kt + 1 < ke;
         typename Loader::Stage st = ld.prep(p);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int ks = q >> 1, rh = q & 1;
+        for (int q = 0; q < PH; ++q) {
+            const int ks = PH == 4 ? q >> 1 : q, rh = PH == 4 ? q & 1 : 0;
             const int fo = ks ? fo1 : fo0;
             // ---- load section
             if (rh == 0) {
@@ -93,31 +101,31 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
                 for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 16 * RB + fo);
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < RT; ++t)
                 fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + (rh * 4 + t) * 16 * RB + fo);
-            if (q < 3 && nxt && !C2D_ABL(p.abl, 1)) {
+            if (q < PH - 1 && nxt && !C2D_ABL(p.abl, 1)) {
 #pragma unroll
                 for (int i = 0; i < PPH; ++i)
                     if (q * PPH + i < P) ld.piece(st, Wn, wave, q * PPH + i);
             }
-            if (q == 3 && nxt) wait_vm_c<0>();   // own pieces of K step kt+1 landed
+            if (q == PH - 1 && nxt) wait_vm_c<0>();   // own pieces of K step kt+1 landed
             // lgkmcnt(0) before the barrier only where the WAR argument needs it (the last
             // reads of this ring slot, phase 3); in phases 0-2 the fragment reads' latency
             // runs under the barrier wait and the compiler's own wait before the first MFMA
             // that uses them (cdna_hip_programming.md 8-phase template: wait after the barrier)
-            if (q == 3 || C2D_PP16_LGKM_ALL)
+            if (q == PH - 1 || C2D_PP16_LGKM_ALL)
                 __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
             C2D_BAR();
             // ---- MFMA section
             if (C2D_ABL(p.abl, 2)) {   // timing ablation: fragments kept live, no MFMA
 #pragma unroll
-                for (int t = 0; t < 4; ++t) asm volatile("" :: "v"(fa[t]));
+                for (int t = 0; t < RT; ++t) asm volatile("" :: "v"(fa[t]));
 #pragma unroll
                 for (int t = 0; t < TN; ++t) asm volatile("" :: "v"(fb[t]));
             } else {
                 __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < RT; ++b)
 #pragma unroll
                     for (int a = 0; a < TN; ++a)
                         acc[a][rh * 4 + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[a], fa[b], acc[a][rh * 4 + b], 0, 0, 0);

@@ -25,7 +25,7 @@
 
 namespace c2d {
 
-template <int NK, bool GG>
+template <int NK, bool GG, int PH>
 __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
     constexpr int TN = 4, TMW = 6, BK = 64, NW = 8;
     constexpr int BM = 2 * TMW * 16, BN = 4 * TN * 16;   // 192 x 256
@@ -33,8 +33,14 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
     typedef M32Loader<BM, BN, BK, NW, 1> Loader;
     constexpr int P = Loader::PMAX, SA = Loader::SA, SB = Loader::SB;
     static_assert(Loader::PMIN == P, "every wave deals the same pieces");
-    constexpr int PPH = (P + 2) / 3;     // pieces per phase, phases 0..2
-    constexpr int NSEC = 4 * NK;         // sections (phases) per tile
+    // PH phases per K step: 4 = (k32 half, row half) with 12-MFMA sections, 2 = k32 half with
+    // 24-MFMA sections (half the barriers, all six A row tiles' fragments live; every DMA piece
+    // of the next K step dealt in phase 0).  L0 GEGLU (K = 320) same box, three alternations:
+    // 172.3-173.7 us with 4 phases, 165.1-166.7 with 2; K = 640 / 1280 keep 4 (2 spills 34 VGPRs)
+    constexpr int RT = PH == 4 ? 3 : 6;
+    static_assert(PH == 2 || PH == 4, "pps phases per K step");
+    constexpr int PPH = (P + PH - 2) / (PH - 1);   // pieces per phase, phases 0..PH-2
+    constexpr int NSEC = PH * NK;        // sections (phases) per tile
     constexpr int NU = GG ? 2 * TMW : TN * TMW;   // stash units: 4 outputs (one 8-B store) per lane
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -117,7 +123,7 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
     C2D_BAR();
     if (wr) C2D_BAR();   // group 1 runs one barrier behind group 0
 
-    f16x8 fa[3], fb[TN];
+    f16x8 fa[RT], fb[TN];
     int base = 0;        // ring slot parity of this tile's K step 0
     for (; tile < ntiles; tile += G) {
         const int next = tile + G;
@@ -137,9 +143,9 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
                 retarget(nm0, nn0);
             }
             typename Loader::Stage st = ld.prep(p);
-            static_for<0, 4>([&](auto qc) __attribute__((always_inline)) {
+            static_for<0, PH>([&](auto qc) __attribute__((always_inline)) {
                 constexpr int q = decltype(qc)::value;
-                constexpr int ks = q >> 1, rh = q & 1, sec = kt * 4 + q;
+                constexpr int ks = PH == 4 ? q >> 1 : q, rh = PH == 4 ? q & 1 : 0, sec = kt * PH + q;
                 const int fo = ks ? fo1 : fo0;
                 // ---- load section
                 if (rh == 0) {
@@ -147,20 +153,20 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
                     for (int t = 0; t < TN; ++t) fb[t] = *reinterpret_cast<const f16x8*>(S + b_base + t * 16 * RB + fo);
                 }
 #pragma unroll
-                for (int t = 0; t < 3; ++t)
+                for (int t = 0; t < RT; ++t)
                     fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + (rh * 3 + t) * 16 * RB + fo);
-                if (q < 3 && nxt) {
+                if (q < PH - 1 && nxt) {
 #pragma unroll
                     for (int i = 0; i < PPH; ++i)
                         if (q * PPH + i < P) ld.piece(st, Wn, wave, q * PPH + i);
                 }
-                if (q == 3 && nxt) wait_vm_c<0>();   // own pieces of the next K step landed
+                if (q == PH - 1 && nxt) wait_vm_c<0>();   // own pieces of the next K step landed
                 __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
                 C2D_BAR();
                 // ---- MFMA section (+ this section's share of the previous tile's stash)
                 __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-                for (int b = 0; b < 3; ++b)
+                for (int b = 0; b < RT; ++b)
 #pragma unroll
                     for (int a = 0; a < TN; ++a)
                         acc[a][rh * 3 + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
@@ -207,13 +213,14 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
 template <int NK, bool GG>
 static void launch_pps(IgemmParams& p, hipStream_t s) {
     constexpr int smem = 2 * (192 + 256) * 128;
+    constexpr int PH = NK == 5 ? 2 : 4;
     static_assert(smem <= 160 * 1024, "LDS ring too large");
-    ensure_lds<igemm_pps_kernel<NK, GG>>(smem);
+    ensure_lds<igemm_pps_kernel<NK, GG, PH>>(smem);
     p.gx = (p.cout + 255) / 256;
     p.gy = (p.M + 191) / 192;
     const int ntiles = p.gx * p.gy;
     const int grid = ntiles < 256 ? ntiles : 256;
-    hipLaunchKernelGGL((igemm_pps_kernel<NK, GG>), dim3(grid), dim3(512), smem, s, p);
+    hipLaunchKernelGGL((igemm_pps_kernel<NK, GG, PH>), dim3(grid), dim3(512), smem, s, p);
 }
 
 // K steps of 64 the unrolled kernel is instantiated for (K = 320 / 640 / 1280: every

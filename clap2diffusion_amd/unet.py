@@ -24,6 +24,10 @@ blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
   Up/Downsample   stride 2 folded into the conv addressing; the nearest x2 upsample
                   materialised by c2d_upsample_nearest2x (one HBM pass) so the 3x3 conv
                   stays on the LDS-DMA path (Upsample2D below).
+  CFG pair        conv_in, the first resnet and the first transformer up to its
+                  cross-attention run once per latent (cfg_pair=True); each producer
+                  writes the first half of a 2N buffer and one device copy fills the
+                  second (forward_nhwc, Transformer2DModel.forward).
 """
 from __future__ import annotations
 
