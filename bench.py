@@ -55,7 +55,7 @@ def measure_dominant_kernel(dev, iters: int = 20):
     for _ in range(2):
         ops.conv(x, wp, kp, c, ksize=3, bias=b, resid=res, out=out)
     tile, split = plans[0]
-    kname = {40: "igemm_pp16_kernel<5,3> 256x320 ping-pong 16x16x32",
+    kname = {40: "igemm_pp16_kernel<5,3,4> 256x320 ping-pong 16x16x32, 4 phases per K step",
              25: "igemm_m32_kernel 256x320 32x32x16"}.get(tile, f"tile {tile}")
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

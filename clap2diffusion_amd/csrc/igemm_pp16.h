@@ -28,7 +28,7 @@
 #pragma once
 
 #ifndef C2D_PP16_PH
-#define C2D_PP16_PH 4
+#define C2D_PP16_PH 0   // 0: per shape family (launch_pp16); 2 / 4 force (A/B builds)
 #endif
 #ifndef C2D_PP16_LGKM_ALL
 #define C2D_PP16_LGKM_ALL 1   // 0: lgkmcnt(0) only in phase 3 (measured neutral: bench 7.845 / 7.840 vs 7.850 / 7.837)
@@ -41,7 +41,7 @@ namespace c2d {
 // accumulator registers of this tile do not fit the AGPR half the allocator grants at two
 // waves per SIMD: with the AGPR-form hint it split them and copied in the loop (40 % slower),
 // and inline-asm "+a" MFMAs computed wrong results (hazards invisible to the compiler).
-template <int TN, int KS>
+template <int TN, int KS, int PH>
 __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
     constexpr int BK = 64, NW = 8, TMW = 8;
     constexpr int BM = 2 * TMW * 16, BN = 4 * TN * 16;
@@ -49,10 +49,12 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
     typedef M32Loader<BM, BN, BK, NW, KS> Loader;
     constexpr int P = Loader::PMAX;
     static_assert(Loader::PMIN == P, "every wave deals the same pieces");
-    // phases per K step: 4 = (k32 half, row half), 20-MFMA sections; 2 = k32 half, 40-MFMA
+    // PH phases per K step: 4 = (k32 half, row half), 20-MFMA sections; 2 = k32 half, 40-MFMA
     // sections (half the barriers; all eight A row tiles' fragments live; every DMA piece of
-    // the next K step dealt in phase 0, so phase 1 is its landing time)
-    constexpr int PH = C2D_PP16_PH, RT = PH == 4 ? 4 : 8;
+    // the next K step dealt in phase 0, so phase 1 is its landing time).  Same box, two
+    // alternations over the c3 shapes (profiles/r03_pp16_phases_ab.txt): 1x1 GEMMs with
+    // K >= 640 and the 256x256 tile 3-4 % faster with 2, the 256x320 3x3 convs within +-0.7 %
+    constexpr int RT = PH == 4 ? 4 : 8;
     static_assert(PH == 2 || PH == 4, "pp16 phases per K step");
     constexpr int PPH = (P + PH - 2) / (PH - 1);   // pieces per phase, phases 0..PH-2
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -206,13 +208,14 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
 
 template <int TN, int KS>
 static void launch_pp16(const IgemmParams& p, hipStream_t s) {
+    constexpr int PH = C2D_PP16_PH ? C2D_PP16_PH : ((KS == 1 || TN == 4) ? 2 : 4);
     constexpr int ring = 2 * (256 + 4 * TN * 16) * 128;
     constexpr int epi_wg = 64 * (4 * TN * 16 + 4) * 4, epi_wv = 8 * 32 * (TN * 16 + 4) * 4;   // epilogue images
     constexpr int epi = epi_wg > epi_wv ? epi_wg : epi_wv;
     constexpr int smem = ring > epi ? ring : epi;
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
-    auto k = igemm_pp16_kernel<TN, KS>;
-    ensure_lds<igemm_pp16_kernel<TN, KS>>(smem);
+    auto k = igemm_pp16_kernel<TN, KS, PH>;
+    ensure_lds<igemm_pp16_kernel<TN, KS, PH>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(512), smem, s, p);
     if (p.ksplit > 1) {
         const size_t total = (size_t)p.M * (p.cout >> 2);
