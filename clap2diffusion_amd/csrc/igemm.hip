@@ -784,7 +784,8 @@ struct DmaPlan { int id, split, nkt; };
 static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int force_split) {
     DmaPlan best = {3, 1, nk};
     double best_t = 1e300;
-    const int splits[] = {1, 2, 3, 4, 6, 8};
+    // 12 / 16 only by a forced plan or the measured table (the cost model is not calibrated there)
+    const int splits[] = {1, 2, 3, 4, 6, 8, 12, 16};
     for (const DmaTile& t : kDmaTiles) {
         if (geglu && !t.geglu) continue;
         if (force_id && t.id != force_id) continue;
@@ -792,6 +793,7 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
         const long tiles = ((M + t.bm - 1) / t.bm) * ((cout + t.bn - 1) / t.bn);
         for (int sp : splits) {
             if (force_split && sp != force_split) continue;
+            if (!force_split && sp > 8) continue;
             if (sp > 1 && (geglu || nk < 8 * sp || tiles >= 256)) continue;
             const int nkt = (nk + sp - 1) / sp;
             const int eff = (nk + nkt - 1) / nkt;
