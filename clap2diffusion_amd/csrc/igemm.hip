@@ -854,8 +854,9 @@ static bool pps_eligible(const c2d_conv_desc* d) {
 // Measured plans for the SD1.5 UNet shapes where the rules below lose >= 3 %: graph-replayed
 // forced-(tile, split) sweeps on MI355X at the three batches the configurations run
 // (scripts/sweep_tiles_graph.py; profiles/r03_sweep_b1.txt, r03_sweep_b4r96.txt,
-// r03_sweep_b8.txt).  The rules are tuned on N = 16 at 64^2; at N = 2 (c1 / c2) every shape is
-// latency bound, and at 96^2 (c5) the 256-row tile count is 288 = 1.1 rounds of 256 CUs.
+// r03_sweep_b8.txt; r03_sweep2.txt: split-K 12 / 16 for the N = 2 small-M convs).  The rules
+// are tuned on N = 16 at 64^2; at N = 2 (c1 / c2) every shape is latency bound, and at 96^2
+// (c5) the 256-row tile count is 288 = 1.1 rounds of 256 CUs.
 // Keyed on (ksize, M = N * H * W, kpad, cout, GEGLU); anything else goes through the rules.
 struct PlanHint { int ksize; long M; int kpad, cout; bool geglu; int id, split; };
 static const PlanHint kPlanHints[] = {
@@ -863,14 +864,16 @@ static const PlanHint kPlanHints[] = {
     {1, 8192, 1280, 320, false, 9, 1},        // ff2 L0: 18.5 -> 17.4 us
     {1, 2048, 640, 1920, false, 9, 1},        // QKV L1: 13.7 -> 13.0
     {1, 512, 1280, 1280, false, 3, 1},        // 1x1 L2: 14.0 -> 10.8
-    {1, 2048, 640, 5120, true, 41, 1},        // GEGLU L1: 32.7 -> 28.9
+    {1, 2048, 640, 5120, true, 50, 1},        // GEGLU L1: 32.7 -> 24.9 (persistent, 220 tiles)
     {3, 8192, 2880, 320, false, 7, 4},        // 3x3 L0 320: 49.3 -> 39.7
     {3, 8192, 5760, 320, false, 40, 6},       // 3x3 L0 640 -> 320: 58.2 -> 54.7
     {3, 8192, 8640, 320, false, 40, 8},       // 3x3 L0 960 -> 320: 72.8 -> 66.9
     {3, 2048, 5760, 640, false, 7, 8},        // 3x3 L1 640: 42.3 -> 38.7
-    {3, 512, 11520, 1280, false, 8, 8},       // 3x3 L2 1280: 55.2 -> 49.7
-    {3, 512, 17280, 1280, false, 9, 8},       // 3x3 L2 1920 -> 1280: 75.2 -> 65.9
-    {3, 512, 23040, 1280, false, 7, 8},       // 3x3 L2 2560 -> 1280: 95.4 -> 80.3
+    {3, 512, 11520, 1280, false, 7, 12},      // 3x3 L2 1280: 55.2 -> 43.7 (split 12)
+    {3, 512, 17280, 1280, false, 41, 16},     // 3x3 L2 1920 -> 1280: 75.2 -> 48.3
+    {3, 512, 23040, 1280, false, 41, 16},     // 3x3 L2 2560 -> 1280: 95.4 -> 57.1
+    {3, 128, 11520, 1280, false, 3, 12},      // 3x3 L3 1280: 31.4 -> 25.7
+    {3, 128, 23040, 1280, false, 9, 16},      // 3x3 L3 2560 -> 1280: 52.6 -> 38.1
     // N = 8, 96^2 (c5)
     {1, 73728, 320, 320, false, 7, 1},        // 1x1 L0: 53.9 -> 41.6
     {1, 73728, 1280, 320, false, 7, 1},       // ff2 L0: 120.7 -> 104.6
@@ -905,7 +908,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
     int id = gemm_tile();
     if (!id) {
         DmaPlan pl;
-        if (plan_hint(ksize, M, kpad, cout, geglu, pl)) return pl;
+        if (plan_hint(ksize, M, kpad, cout, geglu, pl) && (pl.id != 50 || pps_ok)) return pl;
     }
     if (id == 7 && geglu) id = 0;
     if (id == 50) {

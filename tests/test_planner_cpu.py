@@ -26,9 +26,10 @@ def _plan(cin, cout, n, h, k, ws=True, geglu=False):
 @pytest.mark.parametrize("cin,cout,n,h,k,geglu,want", [
     (320, 320, 2, 64, 3, False, (7, 4)),        # c2: L0 resnet conv
     (640, 640, 2, 32, 3, False, (7, 8)),        # c2: L1 resnet conv
-    (2560, 1280, 2, 16, 3, False, (7, 8)),      # c2: L2 up-block conv
+    (2560, 1280, 2, 16, 3, False, (41, 16)),    # c2: L2 up-block conv (split 16)
+    (1280, 1280, 2, 8, 3, False, (3, 12)),      # c2: L3 resnet conv (split 12)
     (1280, 1280, 2, 16, 1, False, (3, 1)),      # c2: L2 projections
-    (640, 5120, 2, 32, 1, True, (41, 1)),       # c2: L1 GEGLU
+    (640, 5120, 2, 32, 1, True, (50, 1)),       # c2: L1 GEGLU (persistent tile)
     (320, 320, 8, 96, 1, False, (7, 1)),        # c5: L0 projections
     (640, 640, 8, 48, 3, False, (41, 1)),       # c5: L1 resnet conv
     (1280, 1280, 16, 16, 1, False, (8, 1)),     # c3: L2 projections (128 x 160, two per CU)
