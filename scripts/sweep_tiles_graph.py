@@ -21,9 +21,10 @@ ap.add_argument("--tiles", default="40,41,25,7,1,2,3,8,9")
 ap.add_argument("--splits", default="1,2,3,4,6,8")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--res", type=int, default=64, help="latent side at level 0")
+ap.add_argument("--vae", action="store_true", help="the VAE decoder's conv shapes (N = --batch)")
 a = ap.parse_args()
 dev = torch.device("cuda")
-N = 2 * a.batch
+N = a.batch if a.vae else 2 * a.batch
 SHAPES = [  # name, ksize, h (latent side at that level), cin, cout, resid, temb
     ("L0 1x1 320 +res", 1, 64, 320, 320, True, False),
     ("L0 1x1 320", 1, 64, 320, 320, False, False),
@@ -54,6 +55,20 @@ SHAPES = [  # name, ksize, h (latent side at that level), cin, cout, resid, temb
     ("L2 geglu 1280->10240", 1, 16, 1280, 10240, False, False),
     ("L0 geglu 320->2560", 1, 64, 320, 2560, False, False),
 ]
+VAE_SHAPES = [  # AutoencoderKL decoder convs (SD1.5: 512 / 512 / 256 / 128 channels at 64 / 128 / 256 / 512^2)
+    ("VAE 64^2 3x3 512 +res", 3, 64, 512, 512, True, False),
+    ("VAE 128^2 3x3 512 +res", 3, 128, 512, 512, True, False),
+    ("VAE 256^2 3x3 512", 3, 256, 512, 512, False, False),
+    ("VAE 256^2 3x3 512->256", 3, 256, 512, 256, False, False),
+    ("VAE 256^2 3x3 256 +res", 3, 256, 256, 256, True, False),
+    ("VAE 512^2 3x3 256", 3, 512, 256, 256, False, False),
+    ("VAE 512^2 3x3 256->128", 3, 512, 256, 128, False, False),
+    ("VAE 512^2 3x3 128 +res", 3, 512, 128, 128, True, False),
+    ("VAE 512^2 1x1 256->128 +res", 1, 512, 256, 128, True, False),
+    ("VAE 256^2 1x1 512->256 +res", 1, 256, 512, 256, True, False),
+]
+if a.vae:
+    SHAPES = VAE_SHAPES
 TILES = [int(t) for t in a.tiles.split(",")]
 SPLITS = [int(s) for s in a.splits.split(",")]
 
@@ -89,7 +104,7 @@ print(f"N = {N}, graph-replayed x{a.iters}", flush=True)
 for name, k, h, cin, cout, res, tmb in SHAPES:
     if a.only and a.only not in name:
         continue
-    h = h * a.res // 64
+    h = h if a.vae else h * a.res // 64
     geglu = "geglu" in name
     x = torch.randn(N, h, h, cin, device=dev, dtype=torch.float16)
     w = torch.randn(cout, cin, k, k, device=dev) / math.sqrt(k * k * cin)
