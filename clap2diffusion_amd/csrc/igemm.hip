@@ -889,6 +889,9 @@ static const PlanHint kPlanHints[] = {
     {1, 4096, 1280, 1280, false, 8, 1},       // 1x1 L2: 27.2 -> 24.5
     {1, 1024, 1280, 1280, false, 3, 1},       // 1x1 mid: 18.9 -> 13.5
     {3, 1024, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 97.2 -> 91.3
+    // VAE decoder at batch 8 (profiles/r03_sweep_vae.txt): only the 1x1 shortcuts gain
+    {1, 2097152, 256, 128, false, 1, 1},      // 512^2 256 -> 128: 511.9 -> 459.4
+    {1, 524288, 512, 256, false, 1, 1},       // 256^2 512 -> 256: 307.5 -> 294.3
 };
 
 static bool plan_hint(int ksize, long M, int kpad, int cout, bool geglu, DmaPlan& pl) {

@@ -34,6 +34,7 @@ def _plan(cin, cout, n, h, k, ws=True, geglu=False):
     (640, 640, 8, 48, 3, False, (41, 1)),       # c5: L1 resnet conv
     (1280, 1280, 16, 16, 1, False, (8, 1)),     # c3: L2 projections (128 x 160, two per CU)
     (1280, 1280, 16, 8, 1, False, (3, 1)),      # c3: mid-block projections
+    (256, 128, 8, 512, 1, False, (1, 1)),       # VAE decoder 512^2 shortcut
 ])
 def test_plan_table_routes_unet_shapes(cin, cout, n, h, k, geglu, want):
     assert _plan(cin, cout, n, h, k, geglu=geglu) == want
