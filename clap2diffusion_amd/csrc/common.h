@@ -12,6 +12,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -117,6 +118,21 @@ __device__ __forceinline__ float gelu_sig(float x) {
     const float x2 = xc * xc;
     const float z = xc * fmaf(fmaf(-0.0009763994f, x2, 0.10652431f), x2, 2.3013635f);   // (a, b, c) * log2 e
     return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-z));
+}
+// h * gelu_sig(g) on two lanes' worth of values at once: the polynomial and the products on
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two results per issue), the clamp,
+// exp2 and rcp per element -- same formula and coefficients as gelu_sig
+__device__ __forceinline__ f32x2 geglu2(f32x2 h, f32x2 g) {
+    const f32x2 xc = {__builtin_amdgcn_fmed3f(g.x, -8.0f, 8.0f), __builtin_amdgcn_fmed3f(g.y, -8.0f, 8.0f)};
+    const f32x2 x2 = xc * xc;
+    f32x2 q = __builtin_elementwise_fma(x2, (f32x2){0.0009763994f, 0.0009763994f},
+                                        (f32x2){-0.10652431f, -0.10652431f});
+    q = __builtin_elementwise_fma(q, x2, (f32x2){-2.3013635f, -2.3013635f});
+    const f32x2 nz = xc * q;   // -z
+    f32x2 e = {__builtin_amdgcn_exp2f(nz.x), __builtin_amdgcn_exp2f(nz.y)};
+    e = e + (f32x2){1.0f, 1.0f};
+    const f32x2 hg = h * g;
+    return hg * (f32x2){__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
 }
 
 

@@ -639,42 +639,78 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
 
 #if C2D_PART(0)
 // split-K combine + epilogue: out[m, j..j+3] = act(sum_s ws[s][m][j..] + bias) + temb + resid
-// (same operation order as epilogue_tiles; slices summed in fixed order)
+// (same operation order as epilogue_tiles; slices summed in fixed order s = 0, 1, ...).
+// KS > 0: the slice count is a compile-time constant and every slab load of an output
+// quad is issued before the first add -- the runtime-count loop waited vmcnt(0) after
+// each slab load, ks dependent HBM / MALL round trips per quad (5.6-11.6 us per call at
+// c2's split 12 / 16, profiles/r03e_c2_by_kernel.txt).  KS = 0: any count, four loads
+// in flight per trip.  One quad per thread (no grid-stride trips).
+template <int KS>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
     const int cq = p.cout >> 2;
-    const size_t total = (size_t)p.M * cq;
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)p.M * cq) return;
     const int hw = p.oh * p.ow;
     const size_t slab = (size_t)p.M * p.cout;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int m = (int)(i / cq);
-        const int j = (int)(i - (size_t)m * cq) * 4;
-        const float* src = p.ws + (size_t)m * p.cout + j;
-        f32x4 acc = *reinterpret_cast<const f32x4*>(src);
-        for (int sl = 1; sl < p.ksplit; ++sl) acc += *reinterpret_cast<const f32x4*>(src + sl * slab);
-        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
-        if (p.bias) {
-            const float4 bv = *reinterpret_cast<const float4*>(p.bias + j);
-            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
-        }
-        f16x4 tv, rv;
-        if (p.temb) tv = *reinterpret_cast<const f16x4*>(p.temb + (size_t)(m / hw) * p.temb_ld + j);
-        if (p.resid) rv = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
-        f16x4 o;
+    const int m = (int)(i / cq);
+    const int j = (int)(i - (size_t)m * cq) * 4;
+    const float* src = p.ws + (size_t)m * p.cout + j;
+    float4 bv = {0.f, 0.f, 0.f, 0.f};
+    f16x4 tv = {0, 0, 0, 0}, rv = {0, 0, 0, 0};
+    if (p.bias) bv = *reinterpret_cast<const float4*>(p.bias + j);
+    if (p.temb) tv = *reinterpret_cast<const f16x4*>(p.temb + (size_t)(m / hw) * p.temb_ld + j);
+    if (p.resid) rv = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
+    f32x4 acc;
+    if constexpr (KS > 0) {
+        f32x4 v[KS];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
-            else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
-            else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
-            else if (p.act == C2D_ACT_QUICK_GELU) v[r] = sigmoid_lin(v[r], 1.702f);
-            if (p.temb) v[r] += (float)tv[r];
-            if (p.resid) v[r] += (float)rv[r];
-            o[r] = (f16)v[r];
+        for (int sl = 0; sl < KS; ++sl) v[sl] = *reinterpret_cast<const f32x4*>(src + sl * slab);
+        acc = v[0];
+#pragma unroll
+        for (int sl = 1; sl < KS; ++sl) acc += v[sl];
+    } else {
+        acc = *reinterpret_cast<const f32x4*>(src);
+        int sl = 1;
+        for (; sl + 4 <= p.ksplit; sl += 4) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(src + sl * slab);
+            const f32x4 b = *reinterpret_cast<const f32x4*>(src + (sl + 1) * slab);
+            const f32x4 c = *reinterpret_cast<const f32x4*>(src + (sl + 2) * slab);
+            const f32x4 d = *reinterpret_cast<const f32x4*>(src + (sl + 3) * slab);
+            acc += a; acc += b; acc += c; acc += d;
         }
-        *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+        for (; sl < p.ksplit; ++sl) acc += *reinterpret_cast<const f32x4*>(src + sl * slab);
+    }
+    float v[4] = {acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w};
+    f16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (p.act == C2D_ACT_GELU) v[r] = gelu_f(v[r]);
+        else if (p.act == C2D_ACT_RELU) v[r] = fmaxf(v[r], 0.f);
+        else if (p.act == C2D_ACT_SILU) v[r] = silu_f(v[r]);
+        else if (p.act == C2D_ACT_QUICK_GELU) v[r] = sigmoid_lin(v[r], 1.702f);
+        if (p.temb) v[r] += (float)tv[r];
+        if (p.resid) v[r] += (float)rv[r];
+        o[r] = (f16)v[r];
+    }
+    *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+}
+
+void run_splitk_reduce(const IgemmParams& p, hipStream_t s) {
+    const size_t total = (size_t)p.M * (p.cout >> 2);
+    const dim3 grid((unsigned)((total + 255) / 256)), blk(256);
+    switch (p.ksplit) {
+        case 2: hipLaunchKernelGGL(splitk_reduce_kernel<2>, grid, blk, 0, s, p); break;
+        case 3: hipLaunchKernelGGL(splitk_reduce_kernel<3>, grid, blk, 0, s, p); break;
+        case 4: hipLaunchKernelGGL(splitk_reduce_kernel<4>, grid, blk, 0, s, p); break;
+        case 6: hipLaunchKernelGGL(splitk_reduce_kernel<6>, grid, blk, 0, s, p); break;
+        case 8: hipLaunchKernelGGL(splitk_reduce_kernel<8>, grid, blk, 0, s, p); break;
+        case 12: hipLaunchKernelGGL(splitk_reduce_kernel<12>, grid, blk, 0, s, p); break;
+        case 16: hipLaunchKernelGGL(splitk_reduce_kernel<16>, grid, blk, 0, s, p); break;
+        default: hipLaunchKernelGGL(splitk_reduce_kernel<0>, grid, blk, 0, s, p); break;
     }
 }
 #else
-__global__ void splitk_reduce_kernel(IgemmParams p);
+void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #endif
 
 }  // namespace c2d
@@ -694,11 +730,7 @@ static void launch_dma(const IgemmParams& p, hipStream_t s) {
     auto k = igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>;
     ensure_lds<igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
-    if (p.ksplit > 1) {
-        const size_t total = (size_t)p.M * (p.cout >> 2);
-        const size_t want = (total + 255) / 256;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
-    }
+    if (p.ksplit > 1) run_splitk_reduce(p, s);
 }
 
 template <int BM, int BN, int AMODE>

@@ -525,11 +525,7 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
     auto k = igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE, EACT>;
     ensure_lds<igemm_m32_kernel<WM, WN, TM, TN, BK, STAGES, KS, DB, WPE, EACT>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
-    if (p.ksplit > 1) {
-        const size_t total = (size_t)p.M * (p.cout >> 2);
-        const size_t want = (total + 255) / 256;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
-    }
+    if (p.ksplit > 1) run_splitk_reduce(p, s);
 }
 
 template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int KS, int WPE, bool DIRECT>

@@ -217,11 +217,7 @@ static void launch_pp16(const IgemmParams& p, hipStream_t s) {
     auto k = igemm_pp16_kernel<TN, KS, PH>;
     ensure_lds<igemm_pp16_kernel<TN, KS, PH>>(smem);
     hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(512), smem, s, p);
-    if (p.ksplit > 1) {
-        const size_t total = (size_t)p.M * (p.cout >> 2);
-        const size_t want = (total + 255) / 256;
-        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(256), 0, s, p);
-    }
+    if (p.ksplit > 1) run_splitk_reduce(p, s);
 }
 
 template <int TN>

@@ -100,8 +100,12 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
         const unsigned off = ok ? (unsigned)(2 * (m * p.out_ld + j)) : kOOB;
         f16x4 o;
         if constexpr (GG) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (f16)((float)sh[ua][ub][r] * gelu_sig((float)sg[ua][ub][r]));
+            // packed-pair math (geglu2), three alternations on one box: L0 GEGLU unchanged (161-164
+            // us), L1 144-146 -> 141-142 us (profiles/r03_geglu_pk_ab.txt)
+            const f32x4 hf = __builtin_convertvector(sh[ua][ub], f32x4);
+            const f32x4 gf = __builtin_convertvector(sg[ua][ub], f32x4);
+            const f32x2 lo = geglu2(hf.xy, gf.xy), hi = geglu2(hf.zw, gf.zw);
+            o = __builtin_convertvector(((f32x4){lo.x, lo.y, hi.x, hi.y}), f16x4);
         } else {
             o = sh[ua][ub];
         }

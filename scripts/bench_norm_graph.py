@@ -1,5 +1,6 @@
 """Per-shape GroupNorm(+SiLU) cost as the UNet sees it: 20 c2d_groupnorm calls captured
 in one graph and replayed (no Python launch overhead).  C2D_GN_FUSED_HW selects the path."""
+import os
 import sys
 from pathlib import Path
 
@@ -9,7 +10,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from clap2diffusion_amd import ops  # noqa: E402
 
 dev = torch.device("cuda")
-N = 16
+N = int(os.environ.get("GN_N", "16"))
 SHAPES = [(64, 320, 0), (64, 640, 320), (32, 640, 0), (32, 1280, 640), (16, 1280, 0), (16, 1280, 1280),
           (8, 1280, 0), (8, 1280, 1280)]
 REPS = 20

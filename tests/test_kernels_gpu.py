@@ -165,6 +165,27 @@ def test_every_dma_tile_forced(dev, force_plan, tile, k, split):
     close(nchw(out), ref)
 
 
+@pytest.mark.parametrize("split,ran", [(2, 2), (3, 3), (4, 4), (6, 6), (8, 8), (12, 12), (16, 15)])
+def test_split_k_combine_every_count(dev, force_plan, split, ran):
+    """splitk_reduce_kernel at every slice count the planner produces: the unrolled
+    compile-time counts (2, 3, 4, 6, 8, 12) and the generic loop (16 on K = 180 steps runs
+    15 slices of 12), with bias + time embedding + residual."""
+    n, h, cin, cout = 2, 16, 1280, 640
+    force_plan(7, split)
+    x = gen(n, cin, h, h, seed=81)
+    w = gen(cout, cin, 3, 3, seed=82, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=83)
+    temb = gen(n, cout, seed=84)
+    resid = gen(n, cout, h, h, seed=85)
+    ref = F.conv2d(x, w, b, padding=1) + temb[:, :, None, None] + resid
+    wp, kp = ops.pack_conv_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(nhwc(x).half().to(dev), wp.to(dev), kp, cout, ksize=3, bias=b.float().to(dev),
+                       temb=temb.half().to(dev), resid=nhwc(resid).half().to(dev))
+    assert plans == [(7, ran)], plans
+    close(nchw(out), ref)
+
+
 @pytest.mark.parametrize("n,h,w,cin,cout,act,bias", [
     (3, 61, 61, 320, 2560, "geglu", True),    # K = 320 (5 K steps), 590 tiles: several per workgroup, ragged M
     (16, 64, 64, 320, 960, None, False),      # the L0 QKV shape, 342 x 4 tiles, no bias
@@ -604,6 +625,9 @@ def test_groupnorm_deterministic(dev):
     (3, 16, 128, 0, 32, True, 1e-6),       # VAE-style cpg 4
     (2, 32, 640, 0, 32, True, 1e-5),       # 32^2: stats + apply pipeline
     (16, 64, 320, 0, 32, True, 1e-5),      # level-0 shape: stats + apply pipeline
+    (1, 32, 1280, 1280, 32, True, 1e-5),   # 2560 channels: two chunks per thread, two sources
+    (2, 32, 320, 0, 16, False, 1e-5),      # 16 groups (cpg 20) through the pipeline
+    (2, 48, 640, 0, 64, True, 1e-6),       # 64 groups: two passes of the group-moment fold
 ])
 def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
     x0 = gen(n, c0, h, h, seed=60) + 0.5
