@@ -886,7 +886,8 @@ static bool pps_eligible(const c2d_conv_desc* d) {
 // Measured plans for the SD1.5 UNet shapes where the rules below lose >= 3 %: graph-replayed
 // forced-(tile, split) sweeps on MI355X at the three batches the configurations run
 // (scripts/sweep_tiles_graph.py; profiles/r03_sweep_b1.txt, r03_sweep_b4r96.txt,
-// r03_sweep_b8.txt; r03_sweep2.txt: split-K 12 / 16 for the N = 2 small-M convs).  The rules
+// r03_sweep_b8.txt; r03_sweep2.txt: split-K 12 / 16 for the N = 2 small-M convs;
+// r03_sweep_fold.txt: the K = 5C ff.net.2 + proj_out GEMMs).  The rules
 // are tuned on N = 16 at 64^2; at N = 2 (c1 / c2) every shape is latency bound, and at 96^2
 // (c5) the 256-row tile count is 288 = 1.1 rounds of 256 CUs.
 // Keyed on (ksize, M = N * H * W, kpad, cout, GEGLU); anything else goes through the rules.
@@ -906,6 +907,7 @@ static const PlanHint kPlanHints[] = {
     {3, 512, 23040, 1280, false, 41, 16},     // 3x3 L2 2560 -> 1280: 95.4 -> 57.1
     {3, 128, 11520, 1280, false, 3, 12},      // 3x3 L3 1280: 31.4 -> 25.7
     {3, 128, 23040, 1280, false, 9, 16},      // 3x3 L3 2560 -> 1280: 52.6 -> 38.1
+    {1, 128, 6400, 1280, false, 3, 12},       // ff.net.2 + proj_out fold L3 (K = 5C): 15.0 -> 14.4
     // N = 8, 96^2 (c5)
     {1, 73728, 320, 320, false, 7, 1},        // 1x1 L0: 53.9 -> 41.6
     {1, 73728, 1280, 320, false, 7, 1},       // ff2 L0: 120.7 -> 104.6
@@ -917,10 +919,13 @@ static const PlanHint kPlanHints[] = {
     {3, 18432, 5760, 640, false, 41, 1},      // 3x3 L1 640: 163.0 -> 147.7
     {3, 1152, 11520, 1280, false, 41, 8},     // 3x3 L3 1280: 65.4 -> 61.2
     {3, 1152, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 116.7 -> 96.1
+    {1, 73728, 1600, 320, false, 7, 1},       // ff.net.2 + proj_out fold L0: 145.6 -> 136.9
+    {1, 18432, 3200, 640, false, 41, 1},      // fold L1: 121.9 -> 87.7
     // N = 16, 64^2 (c3)
     {1, 4096, 1280, 1280, false, 8, 1},       // 1x1 L2: 27.2 -> 24.5
     {1, 1024, 1280, 1280, false, 3, 1},       // 1x1 mid: 18.9 -> 13.5
     {3, 1024, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 97.2 -> 91.3
+    {1, 4096, 6400, 1280, false, 7, 2},       // ff.net.2 + proj_out fold L2: 84.7 -> 82.2
     // VAE decoder at batch 8 (profiles/r03_sweep_vae.txt): only the 1x1 shortcuts gain
     {1, 2097152, 256, 128, false, 1, 1},      // 512^2 256 -> 128: 511.9 -> 459.4
     {1, 524288, 512, 256, false, 1, 1},       // 256^2 512 -> 256: 307.5 -> 294.3

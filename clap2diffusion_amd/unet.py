@@ -18,6 +18,11 @@ blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
   Block           LN1 -> fused QKV GEMM -> flash attn -> to_out (+residual);
                   LN2 -> audio cross-attn processor (+residual);
                   LN3 -> GEGLU GEMM (h*gelu(g) epilogue) -> Linear (+residual).
+  FF out fold     ff.net.2 and proj_out are two linear maps with only a residual add
+                  between them: proj_out(h + W2 g + b2) + x = [Wp | Wp W2] [h; g] +
+                  (Wp b2 + bp) + x, one K = 5C GEMM reading h and g from their own
+                  buffers (Transformer2DModel.finalize / forward; C2D_FOLD_FF_OUT=0
+                  keeps the two GEMMs).
   Normalised activations are materialised once per norm (HBM-bound kernels):
   re-normalising inside the consumer GEMM would redo the affine+SiLU in all 9
   taps of a 3x3 conv / every N-tile of a GEMM, which is VALU-bound on CDNA4.
@@ -31,6 +36,8 @@ blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -38,6 +45,9 @@ from . import ops
 from .layers import HConv2d, HGroupNorm, HLayerNorm, HLinear
 from .processor import AttnProcessor
 from .weights import SD15_UNET
+
+# ff.net.2 folded into proj_out (Transformer2DModel): read once at import, A/B switch only
+FOLD_FF_OUT = os.environ.get("C2D_FOLD_FF_OUT", "1") != "0"
 
 
 class Attention(nn.Module):
@@ -144,6 +154,21 @@ class BasicTransformerBlock(nn.Module):
     def forward(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict,
                 encoder_attention_mask: torch.Tensor | None = None,
                 cfg_dup: torch.Tensor | None = None) -> torch.Tensor:
+        """The whole block: attention part (forward_attn) -> LN3 -> GEGLU -> Linear
+        (+residual, in place in h)."""
+        h = self.forward_attn(h, ehs, cross_attention_kwargs, encoder_attention_mask, cfg_dup)
+        b, l, c = h.shape
+        h2 = h.view(b * l, c)
+        self.ff.net[2](self.ff_inner(h2), resid=h2, out=h2)
+        return h
+
+    def ff_inner(self, h2: torch.Tensor) -> torch.Tensor:
+        """GEGLU(LN3(h)) [M, 4C]: the feed-forward up to its output Linear."""
+        return self.ff.net[0].proj(self.norm3(h2), act="geglu")
+
+    def forward_attn(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict,
+                     encoder_attention_mask: torch.Tensor | None = None,
+                     cfg_dup: torch.Tensor | None = None) -> torch.Tensor:
         """h: [B, L, C] fp16 (updated in place by the fused residual epilogues).
         encoder_attention_mask: additive key bias for attn2 (diffusers BasicTransformerBlock).
         cfg_dup: h holds one half of a CFG pair whose halves are identical up to here, and is the
@@ -158,12 +183,7 @@ class BasicTransformerBlock(nn.Module):
                 cfg_dup[:n].copy_(h)
             cfg_dup[n:].copy_(cfg_dup[:n])
             h = cfg_dup
-        h = self._attend(self.attn2, self.norm2(h), h, ehs, encoder_attention_mask, kw)
-        b, l, c = h.shape
-        h2 = h.view(b * l, c)
-        ff1 = self.ff.net[0].proj(self.norm3(h2), act="geglu")
-        self.ff.net[2](ff1, resid=h2, out=h2)
-        return h
+        return self._attend(self.attn2, self.norm2(h), h, ehs, encoder_attention_mask, kw)
 
 
 class Transformer2DModel(nn.Module):
@@ -173,6 +193,34 @@ class Transformer2DModel(nn.Module):
         self.proj_in = HConv2d(c, c, 1)
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(c, heads, cross_dim)])
         self.proj_out = HConv2d(c, c, 1)
+        # [Wp | Wp W2] packed for the K = 5C GEMM over [h; GEGLU(LN3(h))] (finalize)
+        self.fold_kpad = ops.kpad_of(5 * c)
+        assert self.fold_kpad == 5 * c and self.proj_out.kpad == c, "fold needs C % 64 == 0"
+        self.register_buffer("w_out_fold", torch.zeros(c, self.fold_kpad, dtype=torch.float16), persistent=False)
+        self.register_buffer("b_out_fold", torch.zeros(c, dtype=torch.float32), persistent=False)
+
+    @torch.no_grad()
+    def finalize(self) -> None:
+        """Fold the feed-forward's output Linear into proj_out (both 1x1 maps on the C
+        channels, only the block residual between them): Wf = Wp W2 in fp32 from the fp16
+        weights, rounded once; bias Wp b2 + bp."""
+        c = self.proj_out.cout
+        wp = self.proj_out.weight[:, :c].float()
+        ff2 = self.transformer_blocks[0].ff.net[2]
+        w2 = ff2.weight[:, :4 * c].float()
+        self.w_out_fold.copy_(torch.cat([wp, wp @ w2], 1).to(torch.float16))
+        self.b_out_fold.copy_(wp @ ff2.bias.float() + self.proj_out.bias.float())
+
+    def _block_out(self, t: torch.Tensor, x4: torch.Tensor, resid: torch.Tensor) -> torch.Tensor:
+        """Feed-forward + proj_out (+ resid) of the attention-part output t [B, L, C]:
+        proj_out(t + ff(t)) + resid, as one K = 5C GEMM over [t; GEGLU(LN3(t))]."""
+        blk = self.transformer_blocks[0]
+        b, l, c = t.shape
+        t2 = t.view(b * l, c)
+        ff1 = blk.ff_inner(t2)
+        out = ops.conv(t2, self.w_out_fold, self.fold_kpad, c, ksize=1, bias=self.b_out_fold, x2=ff1,
+                       resid=resid.reshape(b * l, c))
+        return out.view(b, x4.shape[1], x4.shape[2], c)
 
     def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None,
                 cfg_dup: torch.Tensor | None = None):
@@ -182,15 +230,22 @@ class Transformer2DModel(nn.Module):
         duplicates are one device copy of a half each -- a torch.cat of the halves read 1 and
         wrote 2 half-tensors (30 us per call at level 0)."""
         n, hh, ww, c = x.shape
+        blk = self.transformer_blocks[0]
         if cfg_dup is None:
             h = self.proj_in(self.norm.apply(x))
-            t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs,
-                                           encoder_attention_mask)
+            if FOLD_FF_OUT:
+                t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
+                return self._block_out(t, x, x)
+            t = blk(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
             return self.proj_out(t.view(n, hh, ww, c), resid=x)
         hb = x.new_empty((2 * n, hh * ww, c))
         h = self.proj_in(self.norm.apply(x), out=hb[:n].view(n, hh, ww, c))
-        t = self.transformer_blocks[0](h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
-                                       cfg_dup=hb)
+        if FOLD_FF_OUT:
+            t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
+                                 cfg_dup=hb)
+            cfg_dup[n:].copy_(cfg_dup[:n])
+            return self._block_out(t, cfg_dup, cfg_dup)
+        t = blk(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask, cfg_dup=hb)
         cfg_dup[n:].copy_(cfg_dup[:n])
         return self.proj_out(t.view(2 * n, hh, ww, c), resid=cfg_dup)
 
@@ -344,7 +399,7 @@ class UNet2DConditionModel(nn.Module):
     @torch.no_grad()
     def finalize(self) -> None:
         for m in self.modules():
-            if isinstance(m, Attention):
+            if isinstance(m, (Attention, Transformer2DModel)):
                 m.finalize()
         rs = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
         self.w_temb_all.copy_(torch.cat([r.time_emb_proj.weight for r in rs], 0))

@@ -54,6 +54,11 @@ SHAPES = [  # name, ksize, h (latent side at that level), cin, cout, resid, temb
     ("L1 geglu 640->5120", 1, 32, 640, 5120, False, False),
     ("L2 geglu 1280->10240", 1, 16, 1280, 10240, False, False),
     ("L0 geglu 320->2560", 1, 64, 320, 2560, False, False),
+    # ff.net.2 folded into proj_out: K = C (h) + 4C (GEGLU out, a second source), + residual
+    ("L0 fold 320+1280->320 +res", 1, 64, 320, 320, True, False, 1280),
+    ("L1 fold 640+2560->640 +res", 1, 32, 640, 640, True, False, 2560),
+    ("L2 fold 1280+5120->1280 +res", 1, 16, 1280, 1280, True, False, 5120),
+    ("L3 fold 1280+5120->1280 +res", 1, 8, 1280, 1280, True, False, 5120),
 ]
 VAE_SHAPES = [  # AutoencoderKL decoder convs (SD1.5: 512 / 512 / 256 / 128 channels at 64 / 128 / 256 / 512^2)
     ("VAE 64^2 3x3 512 +res", 3, 64, 512, 512, True, False),
@@ -101,19 +106,21 @@ def graph_us(fn, iters):
 
 
 print(f"N = {N}, graph-replayed x{a.iters}", flush=True)
-for name, k, h, cin, cout, res, tmb in SHAPES:
+for name, k, h, cin, cout, res, tmb, *c1 in SHAPES:
     if a.only and a.only not in name:
         continue
+    c1 = c1[0] if c1 else 0
     h = h if a.vae else h * a.res // 64
     geglu = "geglu" in name
     x = torch.randn(N, h, h, cin, device=dev, dtype=torch.float16)
-    w = torch.randn(cout, cin, k, k, device=dev) / math.sqrt(k * k * cin)
+    x2 = torch.randn(N, h, h, c1, device=dev, dtype=torch.float16) if c1 else None
+    w = torch.randn(cout, cin + c1, k, k, device=dev) / math.sqrt(k * k * (cin + c1))
     b = torch.randn(cout, device=dev)
     r = torch.randn(N, h, h, cout, device=dev, dtype=torch.float16) if res else None
     te = torch.randn(N, cout, device=dev, dtype=torch.float16) if tmb else None
     wp, kp = ops.pack_conv_weight(w)
     out = torch.empty(N, h, h, cout // 2 if geglu else cout, device=dev, dtype=torch.float16)
-    fn = lambda: ops.conv(x, wp, kp, cout, ksize=k, bias=b, resid=r, temb=te, out=out,  # noqa: E731
+    fn = lambda: ops.conv(x, wp, kp, cout, ksize=k, bias=b, x2=x2, resid=r, temb=te, out=out,  # noqa: E731
                           act="geglu" if geglu else None)
     with ops.force_plan(0, 0):
         with ops.record_conv_plans() as pl:

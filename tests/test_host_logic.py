@@ -11,7 +11,7 @@ from clap2diffusion_amd.htsat import _row_map, _shift_mask
 from clap2diffusion_amd.processor import AudioAttnProcessor, AudioProcessorManager
 from clap2diffusion_amd.scheduler import DDIMScheduler
 from clap2diffusion_amd.text_encoder import prompt_to_ids
-from clap2diffusion_amd.unet import UNet2DConditionModel
+from clap2diffusion_amd.unet import Transformer2DModel, UNet2DConditionModel
 from clap2diffusion_amd.weights import param_count, unet_param_shapes, vae_decoder_param_shapes
 from oracle import ddim_ref
 from oracle.htsat_ref import shift_mask
@@ -65,6 +65,24 @@ def test_conv_weight_packing_matches_im2col():
     cols = cols.view(24, 9, -1).permute(1, 0, 2).reshape(216, -1)  # -> (tap, cin) order
     y = (wp[:, :216].float() @ cols).view(1, 16, 5, 5)
     assert torch.allclose(y, F.conv2d(x, w, padding=1), atol=2e-2, rtol=2e-2)
+
+
+def test_ff_out_fold_matches_two_linears():
+    """Transformer2DModel.finalize: proj_out(h + ff.net.2(g)) + x == [Wp | Wp W2] [h; g] + (Wp b2 + bp)
+    + x, the K = 5C GEMM the folded forward runs (weights as packed, fp16)."""
+    c = 64
+    t = Transformer2DModel(c, 2, 32, groups=8)
+    g = torch.Generator().manual_seed(3)
+    t.proj_out.load(torch.randn(c, c, 1, 1, generator=g) / 8, torch.randn(c, generator=g))
+    ff2 = t.transformer_blocks[0].ff.net[2]
+    ff2.load(torch.randn(c, 4 * c, generator=g) / 16, torch.randn(c, generator=g))
+    t.finalize()
+    assert t.w_out_fold.shape == (c, 5 * c) and t.fold_kpad == 5 * c
+    h, ff1, x = (torch.randn(5, k, generator=g) for k in (c, 4 * c, c))
+    wp, w2 = t.proj_out.weight.float(), ff2.weight.float()
+    two = (h + ff1 @ w2.T + ff2.bias) @ wp.T + t.proj_out.bias + x
+    one = torch.cat([h, ff1], 1) @ t.w_out_fold.float().T + t.b_out_fold + x
+    assert torch.allclose(one, two, rtol=2e-3, atol=2e-3), (one - two).abs().max()
 
 
 def test_geglu_interleave_roundtrip():

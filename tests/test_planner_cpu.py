@@ -35,6 +35,9 @@ def _plan(cin, cout, n, h, k, ws=True, geglu=False):
     (1280, 1280, 16, 16, 1, False, (8, 1)),     # c3: L2 projections (128 x 160, two per CU)
     (1280, 1280, 16, 8, 1, False, (3, 1)),      # c3: mid-block projections
     (256, 128, 8, 512, 1, False, (1, 1)),       # VAE decoder 512^2 shortcut
+    (6400, 1280, 16, 16, 1, False, (7, 2)),     # c3: L2 ff.net.2 + proj_out fold (K = 5C)
+    (3200, 640, 8, 48, 1, False, (41, 1)),      # c5: L1 fold
+    (6400, 1280, 2, 8, 1, False, (3, 12)),      # c2: L3 fold
 ])
 def test_plan_table_routes_unet_shapes(cin, cout, n, h, k, geglu, want):
     assert _plan(cin, cout, n, h, k, geglu=geglu) == want

@@ -63,6 +63,28 @@ def test_unet_step_matches_oracle(dev, unet_pair, hw, t):
     assert err <= 1e-2, f"eps rel-L2 {err:.3e}"
 
 
+@pytest.mark.parametrize("n,hw", [(2, 32), (16, 16)])
+def test_ff_out_fold_matches_two_gemms(dev, unet_pair, monkeypatch, n, hw):
+    """The K = 5C GEMM over [h; GEGLU] (ff.net.2 folded into proj_out) against the two GEMMs it
+    replaces, same inputs: differences are fp16 rounding only (one rounding of h_ff skipped,
+    Wp W2 rounded once).  Each form is also held to the oracle by the tests above."""
+    import clap2diffusion_amd.unet as U
+    hip, _, mgr = unet_pair
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, 4, hw, hw, generator=g).to(dev)
+    ehs = torch.randn(n, 77, 768, generator=g).to(dev)
+    audio = {lv: (torch.randn(n, 10, 768, generator=g) * 0.5).to(dev) for lv in ("early", "mid", "late")}
+    outs = {}
+    for fold in (False, True):
+        monkeypatch.setattr(U, "FOLD_FF_OUT", fold)
+        with torch.no_grad():
+            outs[fold] = hip(x, 641, ehs, cross_attention_kwargs=mgr.get_audio_kwargs(audio)).sample.float()
+    torch.cuda.synchronize()
+    err = ((outs[True] - outs[False]).norm() / outs[False].norm()).item()
+    parity_log.record(rel_l2=err, tol_l2=3e-3)
+    assert torch.isfinite(outs[True]).all() and err <= 3e-3, f"fold vs two GEMMs rel-L2 {err:.3e}"
+
+
 def test_unet_without_audio_and_batch4(dev, unet_pair):
     hip, ref, mgr = unet_pair
     g = torch.Generator().manual_seed(7)
