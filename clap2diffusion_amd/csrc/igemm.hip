@@ -51,11 +51,23 @@ struct IgemmParams {
     int gx, gy;  // tiles along cout / M
     int ksplit;  // K slices per output tile (DMA path; 1 = no split)
     int nkt;     // K steps per slice
-    float* ws;   // split-K fp32 partials [ksplit][M][cout]
+    float* ws;   // split-K partials [ksplit][M][cout]: fp32, or fp16 when slab16
+    int slab16;  // split-K partials stored as fp16 (C2D_SPLITK_F16): half the slab write + combine read
     int abl;     // timing ablation bits (C2D_GEMM_ABL; 0 in production)
     int lds_epi; // 32x32 kernels: 1 = LDS-staged epilogue (C2D_GEMM_LDSEPI or alignment), 0 = direct
     int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_GEMM_KORDER, default 1)
 };
+
+// one accumulator quad of K slice `slice` into the split-K workspace, fp32 or rounded to fp16
+__device__ __forceinline__ void store_partial(const IgemmParams& p, int slice, int m, int j, const f32x4& v) {
+    const size_t off = ((size_t)slice * p.M + m) * p.cout + j;
+    if (p.slab16) {
+        const f16x4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+        *reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.ws) + off) = h;
+    } else {
+        *reinterpret_cast<f32x4*>(p.ws + off) = v;
+    }
+}
 
 }  // namespace c2d
 #include "epilogue.h"
@@ -600,14 +612,13 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     if (p.ksplit > 1) {
         // raw fp32 partial sums; bias / act / temb / residual go in splitk_reduce_kernel
         const int mw0 = m0 + wm * TM * 16, nw0 = n0 + wn * TN * 16;
-        float* dst = p.ws + (size_t)slice * p.M * p.cout;
 #pragma unroll
         for (int b = 0; b < TM; ++b) {
             const int m = mw0 + b * 16 + (lane & 15);
 #pragma unroll
             for (int a = 0; a < TN; ++a) {
                 const int j = nw0 + a * 16 + 4 * (lane >> 4);
-                if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = acc[a][b];
+                if (m < p.M && j < p.cout) store_partial(p, slice, m, j, acc[a][b]);
             }
         }
         return;
@@ -645,7 +656,18 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
 // each slab load, ks dependent HBM / MALL round trips per quad (5.6-11.6 us per call at
 // c2's split 12 / 16, profiles/r03e_c2_by_kernel.txt).  KS = 0: any count, four loads
 // in flight per trip.  One quad per thread (no grid-stride trips).
-template <int KS>
+// S16: fp16 partials (IgemmParams::slab16), converted and summed in fp32.
+template <bool S16>
+__device__ __forceinline__ f32x4 slab_quad(const float* ws, size_t off) {
+    if constexpr (S16) {
+        const f16x4 h = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(ws) + off);
+        return (f32x4){(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    } else {
+        return *reinterpret_cast<const f32x4*>(ws + off);
+    }
+}
+
+template <int KS, bool S16>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
     const int cq = p.cout >> 2;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -654,7 +676,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
     const size_t slab = (size_t)p.M * p.cout;
     const int m = (int)(i / cq);
     const int j = (int)(i - (size_t)m * cq) * 4;
-    const float* src = p.ws + (size_t)m * p.cout + j;
+    const size_t src = (size_t)m * p.cout + j;
     float4 bv = {0.f, 0.f, 0.f, 0.f};
     f16x4 tv = {0, 0, 0, 0}, rv = {0, 0, 0, 0};
     if (p.bias) bv = *reinterpret_cast<const float4*>(p.bias + j);
@@ -664,21 +686,21 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
     if constexpr (KS > 0) {
         f32x4 v[KS];
 #pragma unroll
-        for (int sl = 0; sl < KS; ++sl) v[sl] = *reinterpret_cast<const f32x4*>(src + sl * slab);
+        for (int sl = 0; sl < KS; ++sl) v[sl] = slab_quad<S16>(p.ws, src + sl * slab);
         acc = v[0];
 #pragma unroll
         for (int sl = 1; sl < KS; ++sl) acc += v[sl];
     } else {
-        acc = *reinterpret_cast<const f32x4*>(src);
+        acc = slab_quad<S16>(p.ws, src);
         int sl = 1;
         for (; sl + 4 <= p.ksplit; sl += 4) {
-            const f32x4 a = *reinterpret_cast<const f32x4*>(src + sl * slab);
-            const f32x4 b = *reinterpret_cast<const f32x4*>(src + (sl + 1) * slab);
-            const f32x4 c = *reinterpret_cast<const f32x4*>(src + (sl + 2) * slab);
-            const f32x4 d = *reinterpret_cast<const f32x4*>(src + (sl + 3) * slab);
+            const f32x4 a = slab_quad<S16>(p.ws, src + sl * slab);
+            const f32x4 b = slab_quad<S16>(p.ws, src + (sl + 1) * slab);
+            const f32x4 c = slab_quad<S16>(p.ws, src + (sl + 2) * slab);
+            const f32x4 d = slab_quad<S16>(p.ws, src + (sl + 3) * slab);
             acc += a; acc += b; acc += c; acc += d;
         }
-        for (; sl < p.ksplit; ++sl) acc += *reinterpret_cast<const f32x4*>(src + sl * slab);
+        for (; sl < p.ksplit; ++sl) acc += slab_quad<S16>(p.ws, src + sl * slab);
     }
     float v[4] = {acc[0] + bv.x, acc[1] + bv.y, acc[2] + bv.z, acc[3] + bv.w};
     f16x4 o;
@@ -698,16 +720,20 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
 void run_splitk_reduce(const IgemmParams& p, hipStream_t s) {
     const size_t total = (size_t)p.M * (p.cout >> 2);
     const dim3 grid((unsigned)((total + 255) / 256)), blk(256);
+#define C2D_SKR(KS)                                                                   \
+    if (p.slab16) hipLaunchKernelGGL((splitk_reduce_kernel<KS, true>), grid, blk, 0, s, p); \
+    else hipLaunchKernelGGL((splitk_reduce_kernel<KS, false>), grid, blk, 0, s, p)
     switch (p.ksplit) {
-        case 2: hipLaunchKernelGGL(splitk_reduce_kernel<2>, grid, blk, 0, s, p); break;
-        case 3: hipLaunchKernelGGL(splitk_reduce_kernel<3>, grid, blk, 0, s, p); break;
-        case 4: hipLaunchKernelGGL(splitk_reduce_kernel<4>, grid, blk, 0, s, p); break;
-        case 6: hipLaunchKernelGGL(splitk_reduce_kernel<6>, grid, blk, 0, s, p); break;
-        case 8: hipLaunchKernelGGL(splitk_reduce_kernel<8>, grid, blk, 0, s, p); break;
-        case 12: hipLaunchKernelGGL(splitk_reduce_kernel<12>, grid, blk, 0, s, p); break;
-        case 16: hipLaunchKernelGGL(splitk_reduce_kernel<16>, grid, blk, 0, s, p); break;
-        default: hipLaunchKernelGGL(splitk_reduce_kernel<0>, grid, blk, 0, s, p); break;
+        case 2: C2D_SKR(2); break;
+        case 3: C2D_SKR(3); break;
+        case 4: C2D_SKR(4); break;
+        case 6: C2D_SKR(6); break;
+        case 8: C2D_SKR(8); break;
+        case 12: C2D_SKR(12); break;
+        case 16: C2D_SKR(16); break;
+        default: C2D_SKR(0); break;
     }
+#undef C2D_SKR
 }
 #else
 void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
@@ -1119,6 +1145,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.ksplit = 1;
     p.nkt = d->kpad / 64;
     p.ws = nullptr;
+    p.slab16 = tuning().splitk_f16;
     p.abl = gemm_abl();
     p.lds_epi = (gemm_lds_epi() || !epi_direct_ok(d)) ? 1 : 0;
     p.cmajor = gemm_korder();

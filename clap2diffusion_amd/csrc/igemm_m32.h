@@ -481,7 +481,6 @@ igemm_m32_kernel(IgemmParams p) {
         return;
     }
     if (p.ksplit > 1) {
-        float* dst = p.ws + (size_t)slice * p.M * p.cout;
 #pragma unroll
         for (int b = 0; b < TM; ++b) {
             const int m = mw0 + b * 32 + (lane & 31);
@@ -491,7 +490,7 @@ igemm_m32_kernel(IgemmParams p) {
                 for (int g = 0; g < 4; ++g) {
                     const int j = nw0 + a * 32 + g * 8 + 4 * (lane >> 5);
                     f32x4 v = {acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
-                    if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = v;
+                    if (m < p.M && j < p.cout) store_partial(p, slice, m, j, v);
                 }
         }
         return;

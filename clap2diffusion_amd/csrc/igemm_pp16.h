@@ -149,14 +149,13 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
         return;
     }
     if (p.ksplit > 1) {
-        float* dst = p.ws + (size_t)slice * p.M * p.cout;
 #pragma unroll
         for (int b = 0; b < TMW; ++b) {
             const int m = mw0 + b * 16 + (lane & 15);
 #pragma unroll
             for (int a = 0; a < TN; ++a) {
                 const int j = nw0 + a * 16 + 4 * (lane >> 4);
-                if (m < p.M && j < p.cout) *reinterpret_cast<f32x4*>(dst + (size_t)m * p.cout + j) = acc[a][b];
+                if (m < p.M && j < p.cout) store_partial(p, slice, m, j, acc[a][b]);
             }
         }
         return;

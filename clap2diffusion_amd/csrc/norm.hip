@@ -255,20 +255,27 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s
 
 // Single-launch GroupNorm (+ SiLU) for small images: one workgroup owns image n
 // and a chunk of CB channels (whole groups, CB % 8 == 0); L = CB / 8 lanes per
-// pixel row, R = 256 / L rows.  Pass 1 accumulates per-thread shifted moments
+// pixel row, R = NT / L rows.  Pass 1 accumulates per-thread shifted moments
 // (fp32), the block folds them in a fixed order (fp64) -> per-group mean / rstd
 // -> per-channel affine in LDS; pass 2 re-reads the slab (L2 / MALL resident)
 // and writes act(x * scale + shift).  Deterministic; replaces partial + finalize
 // + apply (three launches of a few microseconds each) where the image is small.
-__global__ void __launch_bounds__(256) gn_fused_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
-                                                       int c1, int hw, int cpg, int cb, float eps,
-                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       int silu, f16* __restrict__ out) {
-    __shared__ float red[2 * 2048];            // [R][CB][2], R * CB = 256 * 8
+// NT > 256 folds its rows into the 256-row reduction buffer in NT / 256 (+1) fixed-order
+// phases (row r0 adds into slot r0 % R1 after rows r0 - R1, r0 - 2 R1, ...).  A 1024-thread
+// form for few large images (c2's N = 2 at 64^2 / 32^2, where 256 threads walk ~80 pixel rows
+// each) measured 2x slower than partial + finalize + apply there (13.5 -> 29.7 us at
+// 64^2 x 320, profiles/r03h_ab.txt: 2 x C / CB workgroups cannot pull the bytes); only
+// NT = 256 is launched.
+template <int NT>
+__global__ void __launch_bounds__(NT) gn_fused_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
+                                                      int c1, int hw, int cpg, int cb, float eps,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      int silu, f16* __restrict__ out) {
+    __shared__ float red[2 * 2048];            // [R1][CB][2], R1 * CB <= 256 * 8
     __shared__ double gsum[256], gsq[256];     // per channel of the chunk (CB <= 256)
     __shared__ float aff[2 * 256];             // scale | shift per channel of the chunk
     const int cin = c0 + c1;
-    const int L = cb >> 3, R = 256 / L;
+    const int L = cb >> 3, R = NT / L, R1 = 256 / L;
     const int n = blockIdx.y, cbase = blockIdx.x * cb;
     const int t = threadIdx.x, lane_c = t % L, r0 = t / L;
     const bool active = r0 < R && cbase + lane_c * 8 < cin;
@@ -293,17 +300,27 @@ __global__ void __launch_bounds__(256) gn_fused_kernel(const f16* __restrict__ s
             }
         }
     }
-    if (r0 < R) {
+    const int nph = (R + R1 - 1) / R1;
+    for (int ph = 0; ph < nph; ++ph) {
+        if (r0 < R && r0 / R1 == ph) {
+            float* dst = red + ((r0 - ph * R1) * cb + lane_c * 8) * 2;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            red[(r0 * cb + lane_c * 8 + i) * 2] = sum[i];
-            red[(r0 * cb + lane_c * 8 + i) * 2 + 1] = sq[i];
+            for (int i = 0; i < 8; ++i) {
+                if (ph == 0) {
+                    dst[i * 2] = sum[i];
+                    dst[i * 2 + 1] = sq[i];
+                } else {
+                    dst[i * 2] += sum[i];
+                    dst[i * 2 + 1] += sq[i];
+                }
+            }
         }
+        __syncthreads();
     }
-    __syncthreads();
+    const int rs = R < R1 ? R : R1;   // reduction slots written
     if (t < cb) {
         double a = 0.0, b = 0.0;
-        for (int r = 0; r < R; ++r) { a += (double)red[(r * cb + t) * 2]; b += (double)red[(r * cb + t) * 2 + 1]; }
+        for (int r = 0; r < rs; ++r) { a += (double)red[(r * cb + t) * 2]; b += (double)red[(r * cb + t) * 2 + 1]; }
         gsum[t] = a;
         gsq[t] = b;
     }
@@ -636,6 +653,7 @@ static bool gn_use_fused(int n, int cin, int hw, int groups) {
     return gn_fused_cb(n, cin, groups) > 0 && hw <= gn_fused_max_hw();
 }
 
+
 extern "C" size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups) {
     if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return 0;
     if (gn_use_fused(n, c, hw, groups)) return 0;
@@ -654,7 +672,7 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
     hipStream_t s = (hipStream_t)stream;
     if (gn_use_fused(n, cin, hw, groups)) {
         const int cb = gn_fused_cb(n, cin, groups);
-        hipLaunchKernelGGL(gn_fused_kernel, dim3((cin + cb - 1) / cb, n), dim3(256), 0, s, (const f16*)src0,
+        hipLaunchKernelGGL(gn_fused_kernel<256>, dim3((cin + cb - 1) / cb, n), dim3(256), 0, s, (const f16*)src0,
                            (const f16*)src1, c0, c1, hw, cin / groups, cb, eps, gamma, beta, silu, (f16*)out);
         return check_launch();
     }

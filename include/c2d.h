@@ -97,11 +97,16 @@ typedef struct c2d_conv_desc {
 int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
 
 /*
- * Bytes of fp32 split-K workspace c2d_conv2d_igemm would use for this descriptor
- * (0 = the shape fills the chip without splitting K).  Under-filled GEMMs (the
- * 16x16 / 8x8 UNet levels: 80-160 output tiles on 256 CUs) split K across blocks
- * into [split][m][cout] fp32 slabs that a second, stream-ordered kernel sums in
- * fixed order before the epilogue (deterministic; no atomics).
+ * Bytes of split-K workspace c2d_conv2d_igemm would use for this descriptor
+ * (0 = the shape fills the chip without splitting K; sized for fp32 partials).
+ * Under-filled GEMMs (the 16x16 / 8x8 UNet levels: 80-160 output tiles on 256 CUs)
+ * split K across blocks into [split][m][cout] slabs of partial sums that a second,
+ * stream-ordered kernel adds in fp32 in fixed order before the epilogue
+ * (deterministic; no atomics).  Each partial (the fp32 MFMA sum of its K slice) is
+ * stored rounded to fp16 -- half the slab write and combine read; the output carries
+ * about one more fp16 rounding than a single-pass GEMM (rel-L2 ~2e-4 vs the fp32-slab
+ * form), and a partial beyond the fp16 range (|x| > 65504) saturates to inf.
+ * C2D_SPLITK_F16=0 (read once per process) keeps fp32 partials.
  */
 size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d);
 

@@ -11,7 +11,8 @@ from clap2diffusion_amd import ops  # noqa: E402
 
 dev = torch.device("cuda")
 N = int(os.environ.get("GN_N", "16"))
-SHAPES = [(64, 320, 0), (64, 640, 320), (32, 640, 0), (32, 1280, 640), (16, 1280, 0), (16, 1280, 1280),
+SHAPES = [(64, 320, 0), (64, 320, 320), (64, 640, 320), (32, 640, 0), (32, 640, 320), (32, 640, 640), (32, 1280, 640),
+          (16, 1280, 0), (16, 1280, 1280),
           (8, 1280, 0), (8, 1280, 1280)]
 REPS = 20
 for h, c0, c1 in SHAPES:

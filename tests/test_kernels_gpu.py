@@ -625,9 +625,12 @@ def test_groupnorm_deterministic(dev):
     (3, 16, 128, 0, 32, True, 1e-6),       # VAE-style cpg 4
     (2, 32, 640, 0, 32, True, 1e-5),       # 32^2: stats + apply pipeline
     (16, 64, 320, 0, 32, True, 1e-5),      # level-0 shape: stats + apply pipeline
-    (1, 32, 1280, 1280, 32, True, 1e-5),   # 2560 channels: two chunks per thread, two sources
+    (1, 32, 1280, 1280, 32, True, 1e-5),   # 2560 channels, two sources (wide form: 10 lanes, five phases)
     (2, 32, 320, 0, 16, False, 1e-5),      # 16 groups (cpg 20) through the pipeline
     (2, 48, 640, 0, 64, True, 1e-6),       # 64 groups: two passes of the group-moment fold
+    (2, 64, 320, 0, 32, True, 1e-5),       # c2's level 0 (N <= 2: the 1024-thread single launch)
+    (2, 64, 640, 320, 32, True, 1e-5),     # c2's level-0 up-block concat (cpg 30, seam in a group)
+    (1, 64, 960, 0, 32, False, 1e-6),      # 15 lanes per pixel row (cpg 30): four reduction phases
 ])
 def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
     x0 = gen(n, c0, h, h, seed=60) + 0.5
