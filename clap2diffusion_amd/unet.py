@@ -194,8 +194,9 @@ class Transformer2DModel(nn.Module):
         self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(c, heads, cross_dim)])
         self.proj_out = HConv2d(c, c, 1)
         # [Wp | Wp W2] packed for the K = 5C GEMM over [h; GEGLU(LN3(h))] (finalize)
+        # (the two-source GEMM reads h as whole 64-channel K steps: C % 64 == 0, as in SD1.5)
         self.fold_kpad = ops.kpad_of(5 * c)
-        assert self.fold_kpad == 5 * c and self.proj_out.kpad == c, "fold needs C % 64 == 0"
+        self.fold_ok = c % 64 == 0
         self.register_buffer("w_out_fold", torch.zeros(c, self.fold_kpad, dtype=torch.float16), persistent=False)
         self.register_buffer("b_out_fold", torch.zeros(c, dtype=torch.float32), persistent=False)
 
@@ -204,6 +205,8 @@ class Transformer2DModel(nn.Module):
         """Fold the feed-forward's output Linear into proj_out (both 1x1 maps on the C
         channels, only the block residual between them): Wf = Wp W2 in fp32 from the fp16
         weights, rounded once; bias Wp b2 + bp."""
+        if not self.fold_ok:
+            return
         c = self.proj_out.cout
         wp = self.proj_out.weight[:, :c].float()
         ff2 = self.transformer_blocks[0].ff.net[2]
@@ -231,16 +234,17 @@ class Transformer2DModel(nn.Module):
         wrote 2 half-tensors (30 us per call at level 0)."""
         n, hh, ww, c = x.shape
         blk = self.transformer_blocks[0]
+        fold = FOLD_FF_OUT and self.fold_ok
         if cfg_dup is None:
             h = self.proj_in(self.norm.apply(x))
-            if FOLD_FF_OUT:
+            if fold:
                 t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
                 return self._block_out(t, x, x)
             t = blk(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
             return self.proj_out(t.view(n, hh, ww, c), resid=x)
         hb = x.new_empty((2 * n, hh * ww, c))
         h = self.proj_in(self.norm.apply(x), out=hb[:n].view(n, hh, ww, c))
-        if FOLD_FF_OUT:
+        if fold:
             t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
                                  cfg_dup=hb)
             cfg_dup[n:].copy_(cfg_dup[:n])

@@ -77,7 +77,7 @@ def test_ff_out_fold_matches_two_linears():
     ff2 = t.transformer_blocks[0].ff.net[2]
     ff2.load(torch.randn(c, 4 * c, generator=g) / 16, torch.randn(c, generator=g))
     t.finalize()
-    assert t.w_out_fold.shape == (c, 5 * c) and t.fold_kpad == 5 * c
+    assert t.fold_ok and t.w_out_fold.shape == (c, 5 * c) and t.fold_kpad == 5 * c
     h, ff1, x = (torch.randn(5, k, generator=g) for k in (c, 4 * c, c))
     wp, w2 = t.proj_out.weight.float(), ff2.weight.float()
     two = (h + ff1 @ w2.T + ff2.bias) @ wp.T + t.proj_out.bias + x
