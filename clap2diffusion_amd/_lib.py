@@ -21,7 +21,7 @@ ERRORS = {-1: "C2D_E_ARG", -2: "C2D_E_SHAPE", -3: "C2D_E_ALIGN", -4: "C2D_E_HIP"
 
 # every symbol include/c2d.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "c2d_conv2d_igemm", "c2d_conv2d_igemm_workspace_size", "c2d_conv2d_igemm_plan", "c2d_set_plan_override", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_groupnorm_run_workspace_size", "c2d_groupnorm", "c2d_layernorm_stats",
+    "c2d_conv2d_igemm", "c2d_conv2d_igemm_workspace_size", "c2d_conv2d_igemm_plan", "c2d_set_plan_override", "c2d_get_plan_override", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_groupnorm_run_workspace_size", "c2d_groupnorm", "c2d_layernorm_stats",
     "c2d_layernorm", "c2d_attention_fwd", "c2d_attention_fwd_bias", "c2d_attention_fwd_mask", "c2d_window_attention", "c2d_htsat_mel_patches",
     "c2d_patch_merge_gather", "c2d_row_mean", "c2d_l2_normalize", "c2d_softmax_rows", "c2d_clap_log_mel", "c2d_attention_small", "c2d_pack_weights", "c2d_timestep_embedding",
     "c2d_cfg_ddim_step", "c2d_latent_to_nhwc", "c2d_upsample_nearest2x", "c2d_add", "c2d_last_hip_error", "c2d_version",
@@ -59,6 +59,7 @@ def lib() -> ctypes.CDLL:
         "c2d_conv2d_igemm_workspace_size": ([ctypes.POINTER(ConvDesc)], sz),
         "c2d_conv2d_igemm_plan": ([ctypes.POINTER(ConvDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)], i),
         "c2d_set_plan_override": ([i, i], i),
+        "c2d_get_plan_override": ([ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i),
         "c2d_groupnorm_workspace_size": ([i, i, i], sz),
         "c2d_groupnorm_stats": ([vp, vp, i, i, i, i, i, f, vp, vp, vp, vp, vp, vp], i),
         "c2d_groupnorm_apply": ([vp, vp, i, i, i, i, vp, vp, i, vp, vp], i),

@@ -88,10 +88,16 @@ __device__ __forceinline__ int k_off(int row, int ch) {   // byte offset of 16-B
 // (one slot per tile, staged once) and the workgroup walks `qpb` consecutive 128-query
 // blocks of its (image, head) over them -- the streaming form re-staged K/V and paid
 // the staging latency once per 128 queries for ~6 MFLOP of work.
-// KBIAS: an additive per-key score bias (attention_mask of the processor API, the
-// key-padding form diffusers builds: fp32 kbias[b * kb_ldb + h * kb_ldh + key], natural-
-// log units, added to q.k * scale before the softmax); only with NEGC = false, where s
-// holds the unscaled q.k, so the bias enters as bias / scale.
+// KBIAS: an additive score bias (attention_mask of the processor API: fp32
+// kbias[b * kb_ldb + h * kb_ldh + query * kb_ldq + key], natural-log units, added to
+// q.k * scale before the softmax); only with NEGC = false.  The scores move to the log2
+// domain as they are biased (s = q.k * scale * log2 e + bias * log2 e, kb_mul = log2 e), so
+// no bias is ever multiplied by 1 / scale: a finite bias stays finite (finfo.min * log2 e
+// is clamped to -FLT_MAX, so a row of finfo.min entries is a row of equal scores -> the
+// uniform average of V, as torch gives), -inf stays -inf.  With a bias, the running max
+// starts at -inf, padded keys are -inf (never 1e30-style finite values that could win a
+// row whose real keys are all -inf / finfo.min), exp2 uses 0 for a row max still at -inf
+// (so an all -inf row has p = 0, l = 0 and comes out NaN, as torch's softmax of it does).
 template <int D, bool MASK, bool NEGC, bool RES = false, bool KBIAS = false, int NWV = 4>
 __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(D <= 64 ? ATTN_WPE : 1)))
 attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
@@ -234,7 +240,9 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     for (int dt = 0; dt < C::NDT; ++dt)
 #pragma unroll
         for (int qg = 0; qg < 2; ++qg) acc[dt][qg] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float m_run[2] = {NEGC ? 0.f : -1e30f, NEGC ? 0.f : -1e30f}, l_run[2] = {0.f, 0.f};
+    constexpr float M0 = NEGC ? 0.f : (KBIAS ? -INFINITY : -1e30f);   // running-max start
+    const float sc_l2 = KBIAS ? 1.0f : scale_log2;   // KBIAS: s already in the log2 domain
+    float m_run[2] = {M0, M0}, l_run[2] = {0.f, 0.f};
     f32x4 negm[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 
     for (int t = 0; t < ntiles; ++t) {
@@ -289,7 +297,9 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int key = t * 64 + kg * 16 + g * 4 + r;
-                        s[qg][kg][r] += key < lk ? kbr[key] * kb_mul : 0.f;
+                        const float bb = key < lk ? kbr[key] : -INFINITY;
+                        const float b2 = bb == -INFINITY ? bb : fmaxf(bb * kb_mul, -3.402823466e38f);
+                        s[qg][kg][r] = fmaf(s[qg][kg][r], scale_log2, b2);
                     }
             }
         }
@@ -299,7 +309,7 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int key = t * 64 + kg * 16 + g * 4 + r;
-                    if (key >= lk) { s[0][kg][r] = -1e30f; s[1][kg][r] = -1e30f; }
+                    if (key >= lk) { s[0][kg][r] = KBIAS ? -INFINITY : -1e30f; s[1][kg][r] = KBIAS ? -INFINITY : -1e30f; }
                 }
         }
 
@@ -329,23 +339,25 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
                 }
             } else {
                 const float mx = quad_max(lane_max16(s[qg]));
-                const float m_cand = fmaxf(m_run[qg], mx * scale_log2);
+                const float m_cand = fmaxf(m_run[qg], mx * sc_l2);
                 if (__builtin_amdgcn_ballot_w64(m_cand > m_run[qg] + 8.0f)) {
-                    const float alpha = __builtin_amdgcn_exp2f(m_run[qg] - m_cand);
+                    // (KBIAS: a row whose scores are all -inf so far keeps alpha = 1, its O and l are 0)
+                    const float alpha = (KBIAS && m_cand == -INFINITY) ? 1.0f
+                                                                        : __builtin_amdgcn_exp2f(m_run[qg] - m_cand);
                     m_run[qg] = m_cand;
                     if (!C::SUM_MFMA) l_run[qg] *= alpha;
 #pragma unroll
                     for (int dt = 0; dt < C::NDT; ++dt) acc[dt][qg] *= alpha;
                 }
             }
-            const float m_use = m_run[qg];
+            const float m_use = (KBIAS && m_run[qg] == -INFINITY) ? 0.f : m_run[qg];
             float rs = 0.f;
 #pragma unroll
             for (int kg = 0; kg < 4; ++kg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float pv = NEGC ? __builtin_amdgcn_exp2f(s[qg][kg][r])
-                                          : __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], scale_log2, -m_use));
+                                          : __builtin_amdgcn_exp2f(fmaf(s[qg][kg][r], sc_l2, -m_use));
                     s[qg][kg][r] = pv;
                     if (!C::SUM_MFMA) rs += pv;
                 }
@@ -728,7 +740,7 @@ static bool attn_w8() { return tuning().attn_w8 != 0; }
 static int attn_pipelined() { return tuning().attn_pp; }
 
 // attention with an additive per-key bias: the fma-softmax kernels (resident K/V for
-// lk <= 128, streaming otherwise); the bias is pre-multiplied by 1 / scale
+// lk <= 128, streaming otherwise); the bias enters in log2 units (kb_mul = log2 e)
 template <int D>
 static int launch_attn_bias(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                             int batch, int heads, int lq, int lk, float scale, int kv_div, const float* kbias,
@@ -736,7 +748,7 @@ static int launch_attn_bias(const void* q, int ldq, const void* k, int ldk, cons
     using C = AttnCfg<D>;
     const int nqb = (lq + 127) / 128;
     const int smem = C::K_BYTES + C::V_BYTES;
-    const float sl2 = scale * 1.4426950408889634f, mul = 1.0f / scale;
+    const float sl2 = scale * 1.4426950408889634f, mul = 1.4426950408889634f;
     if (lk <= 128) {
         const long bhs = (long)batch * heads;
         int qpb = (int)((bhs * nqb) / 1024);

@@ -972,7 +972,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
     int id = gemm_tile();
-    if (!id) {
+    if (!id && !gemm_split()) {   // a forced split (tile left to the planner) skips the table
         DmaPlan pl;
         if (plan_hint(ksize, M, kpad, cout, geglu, pl) && (pl.id != 50 || pps_ok)) return pl;
     }

@@ -28,7 +28,7 @@ const Tuning& tuning() {
         t.gemm_mode = env_int("C2D_GEMM_MODE", 0);        // 2: register-staged kernels only (A/B)
         t.gemm_korder = env_int("C2D_GEMM_KORDER", 1);    // 3x3 K order: channel-block outer (1) / tap outer (0)
         t.gemm_lds_epi = env_int("C2D_GEMM_LDSEPI", 1);   // 0: direct 32x32 GEGLU epilogue (A/B)
-        t.splitk_f16 = env_int("C2D_SPLITK_F16", 1) != 0;  // split-K partials in fp16 (0: fp32, A/B)
+        t.splitk_f16 = env_int("C2D_SPLITK_F16", 0) != 0;  // 1: split-K partials in fp16 (A/B only: cancelling partials lose range / precision)
         t.attn_negc = env_int("C2D_ATTN_NEGC", 1);
         t.attn_res = env_int("C2D_ATTN_RES", 1);
         t.attn_w8 = env_int("C2D_ATTN_W8", 1);
@@ -66,6 +66,13 @@ extern "C" int c2d_set_plan_override(int tile_id, int ksplit) {
     if (tile_id < 0 || ksplit < 0 || ksplit > 64) return C2D_E_ARG;
     c2d::g_force_tile.store(tile_id, std::memory_order_relaxed);
     c2d::g_force_split.store(ksplit, std::memory_order_relaxed);
+    return C2D_OK;
+}
+
+extern "C" int c2d_get_plan_override(int* tile_id, int* ksplit) {
+    if (!tile_id || !ksplit) return C2D_E_ARG;
+    *tile_id = c2d::g_force_tile.load(std::memory_order_relaxed);
+    *ksplit = c2d::g_force_split.load(std::memory_order_relaxed);
     return C2D_OK;
 }
 

@@ -138,13 +138,17 @@ class force_plan:
         self.tile, self.split = int(tile), int(split)
 
     def __enter__(self):
+        import ctypes
         from ._lib import check, lib
+        t, sp = ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().c2d_get_plan_override(ctypes.byref(t), ctypes.byref(sp)), "c2d_get_plan_override")
+        self.prev = (t.value, sp.value)   # restored on exit: nested overrides / env sweeps survive
         check(lib().c2d_set_plan_override(self.tile, self.split), "c2d_set_plan_override")
         return self
 
     def __exit__(self, *exc):
         from ._lib import lib
-        lib().c2d_set_plan_override(0, 0)
+        lib().c2d_set_plan_override(*self.prev)
         return False
 
 

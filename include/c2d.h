@@ -102,11 +102,13 @@ int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
  * Under-filled GEMMs (the 16x16 / 8x8 UNet levels: 80-160 output tiles on 256 CUs)
  * split K across blocks into [split][m][cout] slabs of partial sums that a second,
  * stream-ordered kernel adds in fp32 in fixed order before the epilogue
- * (deterministic; no atomics).  Each partial (the fp32 MFMA sum of its K slice) is
- * stored rounded to fp16 -- half the slab write and combine read; the output carries
- * about one more fp16 rounding than a single-pass GEMM (rel-L2 ~2e-4 vs the fp32-slab
- * form), and a partial beyond the fp16 range (|x| > 65504) saturates to inf.
- * C2D_SPLITK_F16=0 (read once per process) keeps fp32 partials.
+ * (deterministic; no atomics).  Partials are fp32 (the MFMA sum of the K slice, unrounded):
+ * K slices whose partials cancel -- each far above the output, e.g. beyond the fp16 range
+ * while the output fits -- combine to the same result as the single-pass GEMM
+ * (tests/test_kernels_gpu.py::test_split_k_cancelling_partials_beyond_fp16).
+ * C2D_SPLITK_F16=1 (A/B only, read once per process) stores them rounded to fp16: half the
+ * slab bytes, but a partial beyond +-65504 becomes inf and cancelling partials lose
+ * 2^-11 of their own magnitude.
  */
 size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d);
 
@@ -128,6 +130,10 @@ int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit);
  * a plan from the environment.  C2D_E_ARG for negative values or ksplit > 64.
  */
 int c2d_set_plan_override(int tile_id, int ksplit);
+
+/* The override c2d_set_plan_override last set ((0, 0) = the planner); lets a scoped
+ * override restore the enclosing one.  C2D_E_ARG for NULL pointers. */
+int c2d_get_plan_override(int* tile_id, int* ksplit);
 
 /*
  * GroupNorm statistics folded with the affine into per-(image, channel) scale /

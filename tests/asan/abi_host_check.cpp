@@ -140,6 +140,11 @@ int main() {
         CHECK(c2d_set_plan_override(7, 0) == C2D_OK);
         CHECK(c2d_conv2d_igemm_plan(&f, &t1, &s1) == C2D_OK && t1 == 7);
         CHECK(c2d_set_plan_override(-1, 0) == C2D_E_ARG && c2d_set_plan_override(1, 65) == C2D_E_ARG);
+        {
+            int t = -1, sp = -1;
+            CHECK(c2d_get_plan_override(&t, &sp) == C2D_OK && t == 7 && sp == 0);
+            CHECK(c2d_get_plan_override(nullptr, &sp) == C2D_E_ARG);
+        }
         CHECK(c2d_set_plan_override(0, 0) == C2D_OK);
         CHECK(c2d_conv2d_igemm_plan(&f, &t1, &s1) == C2D_OK && t1 == t0 && s1 == s0);
     }

@@ -37,7 +37,7 @@ def force_plan():
         fp.__enter__()
         held.append(fp)
     yield _force
-    for fp in held:
+    for fp in reversed(held):   # each restores the override its __enter__ found
         fp.__exit__(None, None, None)
 
 
@@ -184,6 +184,35 @@ def test_split_k_combine_every_count(dev, force_plan, split, ran):
                        temb=temb.half().to(dev), resid=nhwc(resid).half().to(dev))
     assert plans == [(7, ran)], plans
     close(nchw(out), ref)
+
+
+@pytest.mark.parametrize("n,h,cin,cout,tile,split", [
+    (16, 16, 1280, 1280, 0, 0),    # c3's L2 resnet conv at its planned split
+    (16, 8, 1280, 1280, 0, 0),     # c3's L3 conv (planned split)
+    (2, 16, 1280, 640, 7, 4),      # forced split 4 on the 128x320 DMA tile
+    (2, 8, 1280, 1280, 41, 16),    # forced split 16 on the ping-pong 256x256 tile
+])
+def test_split_k_cancelling_partials_beyond_fp16(dev, force_plan, n, h, cin, cout, tile, split):
+    """K slices whose partial sums cancel: channels [0, cin/2) carry weights +B, the rest -B,
+    on inputs offset by +A, so each slice's partial is ~A*B*9*(channels per slice) (> 65504,
+    beyond fp16) while the output -- the sum over all slices -- stays ~1e3 and fits fp16.  The
+    combine must give the single-pass result (fp32 partials; fp16 partials overflow to inf
+    here, or lose 2^-11 of a partial's magnitude)."""
+    if tile:
+        force_plan(tile, split)
+    A, B = 16.0, 10.0
+    sgn = torch.ones(cin)
+    sgn[cin // 2:] = -1.0
+    x = (gen(n, cin, h, h, seed=61) + A).half().float()
+    w = (gen(cout, cin, 3, 3, seed=62, scale=0.05) + B * sgn[None, :, None, None]).half().float()
+    b = gen(cout, seed=63)
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
+    assert ref.abs().max() < 3e4, "output must fit fp16"
+    wp, kp = ops.pack_conv_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(nhwc(x).half().to(dev), wp.to(dev), kp, cout, ksize=3, bias=b.float().to(dev))
+    assert plans and plans[0][1] > 1, f"shape expected to split K: {plans}"
+    close(nchw(out), ref, tol_max=5e-3, tol_l2=2e-3)
 
 
 @pytest.mark.parametrize("n,h,w,cin,cout,act,bias", [
@@ -529,6 +558,42 @@ def test_attention_query_mask(dev, b, h, lq, lk, d, form):
     out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d,
                         key_bias=bias.to(dev))
     close(out, ref)
+
+
+@pytest.mark.parametrize("lk", [77, 128, 200])
+@pytest.mark.parametrize("d", [40, 80])
+def test_attention_fully_masked_rows(dev, lk, d):
+    """Rows with no finite score, against torch softmax(q.k * scale + mask) @ v in float64:
+    all finfo.min -> the uniform average of V; all -inf -> NaN; -inf mixed with finfo.min ->
+    uniform over the finfo.min keys; a single finite key -> that key's V.  lk = 77 / 128: the
+    resident-K/V form (77 with a padded tail tile), 200: the streaming form."""
+    b, h, lq = 2, 2, 40
+    q, k, v = gen(b * lq, h * d, seed=171), gen(b * lk, h * d, seed=172), gen(b * lk, h * d, seed=173)
+    g = torch.Generator().manual_seed(174)
+    bias = torch.randn(b, h, lq, lk, generator=g) * 2.0
+    fmin, ninf = torch.finfo(torch.float32).min, float("-inf")
+    bias[0, 0, 3, :] = fmin
+    bias[1, 1, 7, :] = ninf
+    bias[0, 1, 9, :lk // 2] = ninf
+    bias[0, 1, 9, lk // 2:] = fmin
+    bias[1, 0, 11, :] = ninf
+    bias[1, 0, 11, lk - 1] = 0.0
+    bias[1, 0, 12, :] = fmin
+    bias[1, 0, 12, 0] = -5.0
+    q16, k16, v16 = q.half().float(), k.half().float(), v.half().float()
+    qh = q16.view(b, lq, h, d).transpose(1, 2).double()
+    kh = k16.view(b, lk, h, d).transpose(1, 2).double()
+    vh = v16.view(b, lk, h, d).transpose(1, 2).double()
+    sc = (qh @ kh.transpose(-1, -2)) / math.sqrt(d) + bias.double()
+    ref = (torch.softmax(sc, -1) @ vh).transpose(1, 2).reshape(b * lq, h * d).float()
+    out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d,
+                        key_bias=bias.to(dev)).float().cpu()
+    nan_ref = torch.isnan(ref)
+    assert nan_ref.view(b, lq, h, d)[1, 7, 1].all() and nan_ref.sum() == d, "torch: only the all -inf row is NaN"
+    assert torch.equal(torch.isnan(out), nan_ref), "NaN exactly where torch's softmax gives NaN"
+    uni = vh[0, 0].mean(0).float()
+    assert torch.allclose(out.view(b, lq, h, d)[0, 3, 0], uni, atol=2e-3), "finfo.min row: mean of V"
+    close(out[~nan_ref].view(-1), ref[~nan_ref].view(-1))
 
 
 @pytest.mark.parametrize("d", [40, 80, 160])

@@ -1,7 +1,9 @@
-"""End-to-end parity: identical (audio, prompt, seed) triples
-through the HIP pipeline and the fp32 CPU oracle; 10 DDIM steps, PSNR >= 30 dB
-and mean |diff| <= 3/255 on the uint8 images; 50 steps (B = 1), PSNR >= 25 dB;
-the public API surface runs."""
+"""End-to-end parity: identical (audio, prompt, seed) triples through the HIP pipeline and
+the fp32 CPU oracle, PSNR >= 55 dB and mean |diff| <= 0.25 (uint8 units) on the images at
+10 and 50 DDIM steps (achieved 63-65 dB / 0.02-0.03, profiles/r03g_parity_metrics.tsv: a
+precision regression of a few x fails here).  SURVEY.md §8(c)'s bars -- PSNR >= 30 dB at 10
+steps, >= 25 dB at 50, mean |diff| <= 3/255 -- are the documented floors.  The public API
+surface runs."""
 import math
 
 import pytest
@@ -14,6 +16,9 @@ from tests import parity_log
 
 pytestmark = pytest.mark.gpu
 
+PSNR_MIN = 55.0   # dB, every end-to-end case (achieved 63.1-64.8)
+MAD_MAX = 0.25    # mean |diff| in uint8 units (achieved <= 0.032)
+
 
 @pytest.fixture(scope="module")
 def pipe(dev):
@@ -25,7 +30,7 @@ def psnr(a, b):
     return 99.0 if mse == 0 else 10 * math.log10(255.0 ** 2 / mse)
 
 
-def image_parity(img, ref, psnr_min, mad_max=3.0, **extra):
+def image_parity(img, ref, psnr_min, mad_max=MAD_MAX, **extra):
     """PSNR / mean |diff| (uint8 units) of HIP vs oracle images, recorded, then asserted."""
     p = psnr(img, ref)
     mad = (img.float() - ref.float()).abs().mean().item()
@@ -44,17 +49,17 @@ def test_pipeline_matches_oracle_10_steps(pipe, dev):
     rel = ((lat_hip - lat_ref).norm() / lat_ref.norm()).item()
     parity_log.record(latent_rel_l2=rel, tol_l2=2e-2)
     assert rel < 2e-2, f"final latent rel-L2 {rel:.3e}"
-    image_parity(img, ref, 30.0)
+    image_parity(img, ref, PSNR_MIN)
 
 
 def test_pipeline_matches_oracle_50_steps_batch1(pipe, dev):
-    # config c2's schedule (B = 1, 50 DDIM steps) at 128^2: PSNR >= 25 dB, mean |diff| <= 3/255
+    # config c2's schedule (B = 1, 50 DDIM steps) at 128^2
     mel = pipe.mel_features([synthetic_thunder(9)])
     ids = (tokenize([""], dev), tokenize(["a beach"], dev))
     lat = pipe.initial_latents([9])
     img = pipe.generate_batch(mel, None, 50, 7.5, ids=ids, latents=lat).cpu()
     ref, _ = reference_images(mel.cpu(), ids[0].cpu(), ids[1].cpu(), lat.cpu(), 50)
-    image_parity(img, ref, 25.0)
+    image_parity(img, ref, PSNR_MIN)
 
 
 def test_graph_replay_is_repeatable(pipe, dev):
@@ -84,7 +89,7 @@ def test_reference_api_surface(pipe, tmp_path):
 def test_c1_workload_512_10_steps_from_waveform(pipe, dev, progress):
     # BASELINE.json c1's workload (1 x 512^2, 10 DDIM steps, "Thunder" + "a beach") end to end
     # from the 48 kHz waveform: HIP log-mel -> ... -> VAE against the fp32 oracle pipeline
-    # (oracle log-mel from the same waveform): PSNR >= 30 dB, mean |diff| <= 3/255
+    # (oracle log-mel from the same waveform)
     wave = synthetic_thunder(0)
     mel = pipe.mel_features([wave])
     ids = (tokenize([""], dev), tokenize(["a beach"], dev))
@@ -92,14 +97,14 @@ def test_c1_workload_512_10_steps_from_waveform(pipe, dev, progress):
     img = pipe.generate_batch(mel, None, 10, 7.5, ids=ids, latents=lat).cpu()
     assert img.shape == (1, 512, 512, 3)
     ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 10, progress=progress)
-    image_parity(img, ref, 30.0)
+    image_parity(img, ref, PSNR_MIN)
 
 
 @pytest.mark.timeout(900)
 def test_c5_shape_768_from_waveform(pipe, dev, progress):
     # BASELINE.json c5's shape (768^2 = 96^2 latent: 9216-key self-attention, 48^2 / 24^2 / 12^2
     # levels) end to end from the waveform, 3 DDIM steps (the oracle UNet at 96^2 takes ~10 s
-    # per CFG-pair call): PSNR >= 30 dB, mean |diff| <= 3/255
+    # per CFG-pair call)
     wave = synthetic_thunder(4)
     mel = pipe.mel_features([wave])
     ids = (tokenize([""], dev), tokenize(["a thunderstorm"], dev))
@@ -107,7 +112,7 @@ def test_c5_shape_768_from_waveform(pipe, dev, progress):
     img = pipe.generate_batch(mel, None, 3, 7.5, ids=ids, latents=lat).cpu()
     assert img.shape == (1, 768, 768, 3)
     ref, _ = ReferencePipeline(0).run([wave], ids[0].cpu(), ids[1].cpu(), lat.cpu(), 3, progress=progress)
-    image_parity(img, ref, 30.0)
+    image_parity(img, ref, PSNR_MIN)
 
 
 def test_clap_encoder_checkpoint_is_loaded(dev, tmp_path):
@@ -188,7 +193,7 @@ def test_bench_c3_exact_workload_graphed_vs_eager_and_oracle(dev, progress):
     the bench replays.  (1) Bit-identical to the eager generate_batch on the same inputs
     (images and final latents).  (2) Sample 0 against the fp32 oracle pipeline at 50 steps
     (oracle.pipeline_ref.ReferencePipeline: log-mel -> HTSAT -> projectors -> CLIP -> 50
-    CFG-pair UNet calls -> VAE): PSNR >= 25 dB, mean |diff| <= 3/255."""
+    CFG-pair UNet calls -> VAE): PSNR >= PSNR_MIN, mean |diff| <= MAD_MAX."""
     import numpy as np
     from clap2diffusion_amd import distributed as D
     torch.set_num_threads(min(16, torch.get_num_threads()))
@@ -213,4 +218,4 @@ def test_bench_c3_exact_workload_graphed_vs_eager_and_oracle(dev, progress):
     ref, lat_ref = ReferencePipeline(0).run([inp.audios[0]], inp.ids_uncond[:1].cpu(), inp.ids_cond[:1].cpu(),
                                             inp.latents[:1].cpu(), 50, progress=progress)
     rel = ((lat_g[:1].cpu() - lat_ref).norm() / lat_ref.norm()).item()
-    image_parity(g[:1].cpu(), ref, 25.0, latent_rel_l2=rel)
+    image_parity(g[:1].cpu(), ref, PSNR_MIN, latent_rel_l2=rel)

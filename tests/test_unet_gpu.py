@@ -1,6 +1,8 @@
 """One full UNet denoise call (HIP, fp16) against the fp32 CPU oracle on the
 same synthetic SD1.5 weights, with the audio-injecting processors routed by
-AudioProcessorManager.  Tolerance: eps rel-L2 <= 1e-2."""
+AudioProcessorManager.  Tolerance: eps rel-L2 <= 4e-3 (UNET_TOL, ~3x the achieved 1.2e-3, so a
+kernel-level precision regression of a few x fails here); SURVEY.md §8(c)'s bar, 1e-2, is the
+documented floor."""
 import pytest
 import torch
 import torch.nn as nn
@@ -13,6 +15,8 @@ from oracle.unet_ref import UNetRef
 from tests import parity_log
 
 pytestmark = pytest.mark.gpu
+
+UNET_TOL = 4e-3   # achieved 1.21-1.26e-3 on every case (profiles/r03g_parity_metrics.tsv)
 
 
 @pytest.fixture(scope="module")
@@ -41,7 +45,7 @@ def rel_l2(a, b, record=True):
     a, b = a.float().cpu(), b.float().cpu()
     err = ((a - b).norm() / b.norm()).item()
     if record:
-        parity_log.record(rel_l2=err, tol_l2=1e-2)
+        parity_log.record(rel_l2=err, tol_l2=UNET_TOL)
     return err
 
 
@@ -60,7 +64,7 @@ def test_unet_step_matches_oracle(dev, unet_pair, hw, t):
     torch.cuda.synchronize()
     assert torch.isfinite(e_hip).all()
     err = rel_l2(e_hip, e_ref)
-    assert err <= 1e-2, f"eps rel-L2 {err:.3e}"
+    assert err <= UNET_TOL, f"eps rel-L2 {err:.3e}"
 
 
 @pytest.mark.parametrize("n,hw", [(2, 32), (16, 16)])
@@ -93,7 +97,7 @@ def test_unet_without_audio_and_batch4(dev, unet_pair):
     with torch.no_grad():
         e_ref = ref(x, 261, ehs, None)
         e_hip = hip(x.to(dev), 261, ehs.to(dev)).sample
-    assert rel_l2(e_hip, e_ref) <= 1e-2
+    assert rel_l2(e_hip, e_ref) <= UNET_TOL
 
 
 def test_attn_processor_names_and_levels(unet_pair):
@@ -124,7 +128,7 @@ def test_unet_step_c3_batch_matches_oracle(dev, unet_pair):
     with torch.no_grad():
         e_ref = ref(x, 981, ehs, audio)
     err = rel_l2(e_hip, e_ref)
-    assert err <= 1e-2, f"eps rel-L2 {err:.3e}"
+    assert err <= UNET_TOL, f"eps rel-L2 {err:.3e}"
 
 
 @pytest.mark.timeout(600)
@@ -146,7 +150,7 @@ def test_unet_step_c5_batch_matches_oracle(dev, unet_pair):
     with torch.no_grad():
         e_ref = ref(x, 741, ehs, audio)
     err = rel_l2(e_hip, e_ref)
-    assert err <= 1e-2, f"eps rel-L2 {err:.3e}"
+    assert err <= UNET_TOL, f"eps rel-L2 {err:.3e}"
 
 
 @pytest.mark.parametrize("n,hw", [(16, 64), (2, 32)])
@@ -189,7 +193,7 @@ def test_unet_encoder_attention_mask_matches_oracle(dev, unet_pair):
         e_hip = hip(x.to(dev), 601, ehs.to(dev), encoder_attention_mask=keep.to(dev),
                     cross_attention_kwargs=mgr.get_audio_kwargs({k: v.to(dev) for k, v in audio.items()})).sample
     assert rel_l2(e_nomask, e_ref, record=False) > 5e-2       # the mask matters at this tolerance
-    assert rel_l2(e_hip, e_ref) <= 1e-2
+    assert rel_l2(e_hip, e_ref) <= UNET_TOL
 
 
 class TorchAudioProcessor(nn.Module):
@@ -247,4 +251,4 @@ def test_diffusers_style_torch_processor_in_hip_unet(dev, unet_pair):
         hip.set_attn_processor(saved)
     with torch.no_grad():
         e_ref = ref(x, 421, ehs, audio)
-    assert rel_l2(e_hip, e_ref) <= 1e-2
+    assert rel_l2(e_hip, e_ref) <= UNET_TOL
