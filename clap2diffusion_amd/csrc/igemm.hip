@@ -743,6 +743,7 @@ void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #include "igemm_m32.h"
 #include "igemm_pp16.h"
 #include "igemm_pps.h"
+#include "igemm_pp16r.h"
 namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -792,10 +793,12 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
+C2D_TILE_FN(42);
 #if C2D_PART(1)
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
 C2D_TILE_FN(50) { (void)ksize; (void)cout; run_pps(p, s); }   // persistent 192x256, carried epilogue (1x1)
+C2D_TILE_FN(42) { (void)ksize; (void)cout; run_pp16r<5>(p, s); }   // 256x320 row-ring 3x3 over a zero-bordered source
 #endif
 #if C2D_PART(2)
 C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
@@ -836,6 +839,8 @@ static const DmaTile kDmaTiles[] = {
     // two workgroups per CU (<= 80 KiB of LDS): the under-filled 1x1 / 3x3 shapes
     {8, 128, 160, 2, 0.0f, false},
     {9, 64, 160, 2, 0.0f, false},
+    // row-ring 3x3 over a zero-bordered source (igemm_pp16r.h): chosen by plan_for only
+    {42, 256, 320, 1, 0.0f, false},
 };
 struct DmaPlan { int id, split, nkt; };
 
@@ -968,10 +973,26 @@ static bool plan_hint(int ksize, long M, int kpad, int cout, bool geglu, DmaPlan
     return false;
 }
 
-static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize) {
+// tile 42 plan: split-K slices own whole channel blocks (9 K steps each)
+static DmaPlan rr_plan(int nk, int split) {
+    const int ncb = nk / 9;
+    const int sp = split < 1 ? 1 : (split > ncb ? ncb : split);
+    const int cbs = (ncb + sp - 1) / sp;
+    return {42, (ncb + cbs - 1) / cbs, 9 * cbs};
+}
+
+static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize, bool rr_ok = false) {
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
     int id = gemm_tile();
+    if (id == 42) {
+        if (rr_ok) return rr_plan(nk, gemm_split());
+        id = 0;
+    }
+    // the row-ring 3x3 (tile 42) on a zero-bordered source once its 256 x 320 tiles fill the chip
+    // (c3's level-0 ResnetBlock2D convs); under-filled grids keep the planner's tiles over the
+    // padded image (a valid 3x3, every tap in bounds)
+    if (!id && rr_ok && !gemm_split() && cout % 320 == 0 && (M / 256) * (cout / 320) >= 192) return rr_plan(nk, 1);
     if (!id && !gemm_split()) {   // a forced split (tile left to the planner) skips the table
         DmaPlan pl;
         if (plan_hint(ksize, M, kpad, cout, geglu, pl) && (pl.id != 50 || pps_ok)) return pl;
@@ -1042,6 +1063,7 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
     switch (pl.id) {
+        case 42: return run_tile_42(p, ksize, cout, s);
         case 25: return run_tile_25(p, ksize, cout, s);
         case 40: return run_tile_40(p, ksize, cout, s);
         case 41: return run_tile_41(p, ksize, cout, s);
@@ -1061,17 +1083,24 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
 static bool dma_eligible(const c2d_conv_desc* d) {
     const int cin = d->c0 + d->c1;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
-    const size_t src_bytes = (size_t)d->n * d->h * d->w * (size_t)(d->c0 > d->c1 ? d->c0 : d->c1) * 2;
+    const int pd = d->src_pad ? 2 : 0;
+    const size_t src_bytes = (size_t)d->n * (d->h + pd) * (d->w + pd) * (size_t)(d->c0 > d->c1 ? d->c0 : d->c1) * 2;
     return (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && gemm_mode() != 2 &&
            (d->c1 == 0 || (d->c0 & 63) == 0) && src_bytes < (1u << 31) &&
            (size_t)d->cout * d->kpad * 2 < (1u << 31);  // 32-bit buffer offsets
+}
+
+// the row-ring tile 42 (igemm_pp16r.h) applies to this descriptor
+static bool rr_eligible(const c2d_conv_desc* d) {
+    return d->src_pad && d->pro == C2D_PRO_NONE && pp16r_shape_ok(d->ksize, d->stride, 0, d->c1, d->c0, d->ow, d->oh, d->w + 2) &&
+           d->oh == d->h && d->ow == d->w && d->kpad == 9 * d->c0;
 }
 
 extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
     if (!dma_eligible(d)) return 0;
     const long M = (long)d->n * d->oh * d->ow;
-    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize);
+    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
 
@@ -1084,7 +1113,7 @@ extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* 
         return C2D_OK;
     }
     const long M = (long)d->n * d->oh * d->ow;
-    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize);
+    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
     if (pl.split > 1) {
         const size_t need = (size_t)pl.split * M * d->cout * sizeof(float);
         if (!(d->ws && d->ws_bytes >= need && aligned16(d->ws))) pl.split = 1;
@@ -1118,6 +1147,9 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     if (d->stride != 1 && d->stride != 2) return C2D_E_SHAPE;
     if (d->ksize == 1 && (d->stride != 1 || d->up || d->oh != d->h || d->ow != d->w)) return C2D_E_SHAPE;
     if (d->up && d->stride != 1) return C2D_E_SHAPE;
+    // zero-bordered source [n][h + 2][w + 2][c0]: 3x3, stride 1, one source, output h x w
+    if (d->src_pad && (d->ksize != 3 || d->stride != 1 || d->up || d->c1 || d->oh != d->h || d->ow != d->w))
+        return C2D_E_SHAPE;
 
     IgemmParams p;
     p.src0 = (const f16*)d->src0; p.src1 = (const f16*)d->src1;
@@ -1125,7 +1157,9 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.n = d->n; p.h = d->h; p.w = d->w; p.oh = d->oh; p.ow = d->ow;
     p.stride = d->stride; p.up = d->up; p.pad = (d->ksize == 3) ? 1 : 0;
     p.vh = d->up ? 2 * d->h : d->h; p.vw = d->up ? 2 * d->w : d->w;
-    if (d->ksize == 3) {
+    if (d->src_pad) {   // a valid 3x3 over the padded image: every kernel's addressing as is, no halo
+        p.h = d->h + 2; p.w = d->w + 2; p.vh = p.h; p.vw = p.w; p.pad = 0;
+    } else if (d->ksize == 3) {
         int eh = (p.vh + 2 - 3) / d->stride + 1, ew = (p.vw + 2 - 3) / d->stride + 1;
         if (eh != d->oh || ew != d->ow) return C2D_E_SHAPE;
     }
@@ -1151,7 +1185,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize);
+        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
         if (pl.split > 1) {
             const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
             if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {

@@ -206,10 +206,14 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const f16* __restrict_
 // Grid (pixel blocks, image): a thread owns channel chunks lane_c (+ 256 q) of image
 // n, keeps their affine in registers and walks pixels -- no per-chunk index
 // divisions or table reloads.  HBM-bound (2 B read + 2 B written / element).
-template <int CPT>
+// PAD: the output is the zero-bordered layout [n][h + 2][w + 2][c] (w = pw - 2) that the
+// row-ring conv reads (c2d_conv_desc::src_pad): the walk covers the padded pixels, border
+// pixels get zeros, interior ones the normalised input.
+template <int CPT, bool PAD = false>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
                                                        int c1, int hw, const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, int silu, f16* __restrict__ out) {
+                                                       const float* __restrict__ shift, int silu, f16* __restrict__ out,
+                                                       int pw = 0) {
     const int cin = c0 + c1, nch = cin >> 3;
     const int L = nch < 256 ? nch : 256, R = 256 / L;
     const int t = threadIdx.x, lane_c = t % L, r0 = t / L;
@@ -233,6 +237,32 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s
             av[q][i] = scale[(size_t)n * cin + c + i];
             bv[q][i] = shift[(size_t)n * cin + c + i];
         }
+    }
+    if constexpr (PAD) {
+        const int w = pw - 2, ph = hw / w + 2, npix = ph * pw;
+        const size_t pimg = (size_t)n * npix;
+#pragma unroll 2
+        for (int pp = blockIdx.x * R + r0; pp < npix; pp += gridDim.x * R) {
+            const int py = pp / pw, px = pp - py * pw;
+            const bool inner = py >= 1 && py < ph - 1 && px >= 1 && px < pw - 1;
+            const size_t gp = img + (inner ? (py - 1) * w + (px - 1) : 0);
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                if (!on[q]) continue;
+                f16x8 o = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+                if (inner) {
+                    const f16x8 v = *reinterpret_cast<const f16x8*>(src[q] + gp * ld[q]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float y = fmaf((float)v[j], av[q][j], bv[q][j]);
+                        if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                        o[j] = (f16)y;
+                    }
+                }
+                *reinterpret_cast<f16x8*>(out + (pimg + pp) * cin + cc[q]) = o;
+            }
+        }
+        return;
     }
 #pragma unroll 4
     for (int pix = blockIdx.x * R + r0; pix < hw; pix += gridDim.x * R) {
@@ -683,4 +713,41 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
     int rc = c2d_groupnorm_stats(src0, src1, c0, c1, n, hw, groups, eps, gamma, beta, scale, shift, ws, stream);
     if (rc != C2D_OK) return rc;
     return c2d_groupnorm_apply(src0, src1, c0, c1, n, hw, scale, shift, silu, out, stream);
+}
+
+extern "C" size_t c2d_groupnorm_pad_workspace_size(int n, int c, int h, int w) {
+    if (n <= 0 || c <= 0 || h <= 0 || w <= 0) return 0;
+    return c2d_groupnorm_workspace_size(n, c, h * w) + (size_t)n * c * 2 * sizeof(float);
+}
+
+extern "C" int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int c1, int n, int h, int w, int groups,
+                                 float eps, const float* gamma, const float* beta, int silu, void* out, void* ws,
+                                 size_t ws_bytes, void* stream) {
+    if (!src0 || !gamma || !beta || !out || !ws) return C2D_E_ARG;
+    if (c1 > 0 && !src1) return C2D_E_ARG;
+    const int cin = c0 + c1;
+    if ((c0 & 7) || (c1 & 7) || cin <= 0 || groups <= 0 || cin % groups) return C2D_E_SHAPE;
+    if (cin / groups > 256 || n <= 0 || h <= 0 || w <= 0 || (cin >> 3) > 512) return C2D_E_SHAPE;
+    if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out) || !aligned16(ws)) return C2D_E_ALIGN;
+    const int hw = h * w;
+    if (ws_bytes < c2d_groupnorm_pad_workspace_size(n, cin, h, w)) return C2D_E_ARG;
+    const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
+    float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
+    float* shift = scale + (size_t)n * cin;
+    int rc = c2d_groupnorm_stats(src0, src1, c0, c1, n, hw, groups, eps, gamma, beta, scale, shift, ws, stream);
+    if (rc != C2D_OK) return rc;
+    const int nch = cin >> 3;
+    const int L = nch < 256 ? nch : 256, R = 256 / L;
+    const int npix = (h + 2) * (w + 2);
+    int bx = (gn_apply_blocks() + n - 1) / n;
+    const int maxb = (npix + R - 1) / R;
+    if (bx > maxb) bx = maxb;
+    if (bx < 1) bx = 1;
+    if (nch <= 256)
+        hipLaunchKernelGGL((gn_apply_kernel<1, true>), dim3(bx, n), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
+                           (const f16*)src1, c0, c1, hw, scale, shift, silu, (f16*)out, w + 2);
+    else
+        hipLaunchKernelGGL((gn_apply_kernel<2, true>), dim3(bx, n), dim3(256), 0, (hipStream_t)stream, (const f16*)src0,
+                           (const f16*)src1, c0, c1, hw, scale, shift, silu, (f16*)out, w + 2);
+    return check_launch();
 }

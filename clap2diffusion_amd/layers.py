@@ -80,9 +80,11 @@ class HGroupNorm(nn.Module):
     def stats(self, x: torch.Tensor, x2: torch.Tensor | None = None):
         return ops.group_norm_stats(x, self.num_groups, self.eps, self.weight, self.bias, x2=x2)
 
-    def apply(self, x: torch.Tensor, x2: torch.Tensor | None = None, silu: bool = False) -> torch.Tensor:
-        """act(GroupNorm(cat[x, x2])) materialised once (c2d_groupnorm)."""
-        return ops.group_norm(x, self.num_groups, self.eps, self.weight, self.bias, silu, x2=x2)
+    def apply(self, x: torch.Tensor, x2: torch.Tensor | None = None, silu: bool = False,
+              pad: bool = False) -> torch.Tensor:
+        """act(GroupNorm(cat[x, x2])) materialised once (c2d_groupnorm); pad: in the zero-bordered
+        layout a conv(..., padded=True) reads (c2d_groupnorm_pad)."""
+        return ops.group_norm(x, self.num_groups, self.eps, self.weight, self.bias, silu, x2=x2, pad=pad)
 
 
 class HLayerNorm(nn.Module):

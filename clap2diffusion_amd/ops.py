@@ -9,6 +9,7 @@ the calls can be captured into a torch.cuda.CUDAGraph (hipGraph) as is.
 from __future__ import annotations
 
 import ctypes
+import functools
 import math
 
 import torch
@@ -83,10 +84,11 @@ def geglu_interleave(w: torch.Tensor, b: torch.Tensor | None):
 def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: int, bias=None, stride: int = 1,
          up: bool = False, x2: torch.Tensor | None = None, gn=None, gn_silu: bool = False, ln=None,
          silu_in: bool = False, act: str | None = None, temb: torch.Tensor | None = None,
-         resid: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+         resid: torch.Tensor | None = None, out: torch.Tensor | None = None, padded: bool = False) -> torch.Tensor:
     """Implicit-GEMM conv / linear (c2d::conv2d_igemm).
 
-    x: NHWC [N, H, W, C0] fp16 (or 2-D [M, C0] for a linear layer).
+    x: NHWC [N, H, W, C0] fp16 (or 2-D [M, C0] for a linear layer); padded: x is the
+    zero-bordered [N, H + 2, W + 2, C0] of group_norm(pad=True) (3x3, stride 1, one source).
     gn: (scale, shift) fp32 [N, C0+C1]; ln: (stats [M, 2], gamma, beta).
     """
     _require(x, "x")
@@ -94,6 +96,9 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
         h, w = 1, x.shape[0]
     else:
         _, h, w, _ = x.shape
+        if padded:
+            assert ksize == 3 and stride == 1 and not up and x2 is None, "padded source: 3x3, stride 1, one source"
+            h, w = h - 2, w - 2
     assert x.is_contiguous() and x.dtype == F16
     if x2 is not None:
         assert x2.is_contiguous() and x2.dtype == F16 and x2.shape[:-1] == x.shape[:-1]
@@ -112,8 +117,24 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
     gs, gh = gn if gn is not None else (None, None)
     ls, lg, lb = ln if ln is not None else (None, None, None)
     C2D.conv2d_igemm(x, weight, kpad, cout, ksize, stride, up, x2, gs, gh, gn_silu, ls, lg, lb, silu_in, bias,
-                     C2D_ACT[act], temb, resid, out)
+                     C2D_ACT[act], temb, resid, out, bool(padded))
     return out
+
+
+@functools.lru_cache(maxsize=None)
+def rowring_conv(n: int, h: int, w: int, cin: int, cout: int) -> bool:
+    """Does c2d's planner run a 3x3 stride-1 conv (n x h x w, cin -> cout) on the row-ring tile 42
+    when its source is zero-bordered?  (Asked of the library, c2d_conv2d_igemm_plan: the padded
+    layout is worth writing only where that kernel reads it.)"""
+    import ctypes
+    from ._lib import ConvDesc, check, lib
+    d = ConvDesc()
+    d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, n, h, w, h, w, 3, 1
+    d.cout, d.kpad, d.src_pad = cout, kpad_of(9 * cin), 1
+    d.out_ld = cout
+    tid, ks = ctypes.c_int(), ctypes.c_int()
+    check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
+    return tid.value == 42
 
 
 class record_conv_plans:
@@ -144,11 +165,13 @@ class force_plan:
         check(lib().c2d_get_plan_override(ctypes.byref(t), ctypes.byref(sp)), "c2d_get_plan_override")
         self.prev = (t.value, sp.value)   # restored on exit: nested overrides / env sweeps survive
         check(lib().c2d_set_plan_override(self.tile, self.split), "c2d_set_plan_override")
+        rowring_conv.cache_clear()        # the planner's answers change under an override
         return self
 
     def __exit__(self, *exc):
         from ._lib import lib
         lib().c2d_set_plan_override(*self.prev)
+        rowring_conv.cache_clear()
         return False
 
 
@@ -185,11 +208,18 @@ def group_norm_apply(x: torch.Tensor, gn, silu: bool, x2: torch.Tensor | None = 
 
 
 def group_norm(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor, silu: bool,
-               x2: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+               x2: torch.Tensor | None = None, out: torch.Tensor | None = None, pad: bool = False) -> torch.Tensor:
     """act(GroupNorm(cat[x, x2])) in one c2d::groupnorm call (single fused kernel for
-    small images, stats + apply otherwise)."""
+    small images, stats + apply otherwise).  pad: write the zero-bordered layout
+    [N, H + 2, W + 2, C] (c2d::groupnorm_pad) for a conv(..., padded=True)."""
     _require(x, "x")
     c = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    if pad:
+        n, h, w, _ = x.shape
+        if out is None:
+            out = torch.empty((n, h + 2, w + 2, c), device=x.device, dtype=F16)
+        C2D.groupnorm_pad(x, x2, groups, float(eps), gamma, beta, bool(silu), out)
+        return out
     if out is None:
         out = torch.empty((*x.shape[:-1], c), device=x.device, dtype=F16)
     C2D.groupnorm(x, x2, groups, float(eps), gamma, beta, bool(silu), out)

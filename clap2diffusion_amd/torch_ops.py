@@ -24,12 +24,14 @@ _CU = "cuda"
 
 
 def _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma,
-               ln_beta, silu_in, bias, act, temb, resid, out) -> ConvDesc:
+               ln_beta, silu_in, bias, act, temb, resid, out, src_pad=False) -> ConvDesc:
     if x.dim() == 2:
         n, h, w = 1, 1, x.shape[0]
         c0 = x.shape[1]
     else:
         n, h, w, c0 = x.shape
+        if src_pad:   # zero-bordered [n][h + 2][w + 2][c0]: logical size h x w
+            h, w = h - 2, w - 2
     c1 = x2.shape[-1] if x2 is not None else 0
     if ksize == 3:
         vh, vw = (2 * h, 2 * w) if up else (h, w)
@@ -57,6 +59,7 @@ def _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift,
         d.resid = ptr(resid); d.resid_ld = resid.stride(-2) if resid.dim() == 2 else resid.shape[-1]
     d.out = ptr(out)
     d.out_ld = out.stride(-2) if out.dim() == 2 else out.shape[-1]
+    d.src_pad = int(src_pad)
     return d
 
 
@@ -68,10 +71,11 @@ def conv2d_igemm(x: Tensor, weight: Tensor, kpad: int, cout: int, ksize: int, st
                  x2: Optional[Tensor], gn_scale: Optional[Tensor], gn_shift: Optional[Tensor], gn_silu: bool,
                  ln_stats: Optional[Tensor], ln_gamma: Optional[Tensor], ln_beta: Optional[Tensor], silu_in: bool,
                  bias: Optional[Tensor], act: int, temb: Optional[Tensor], resid: Optional[Tensor],
-                 out: Tensor) -> None:
-    """c2d_conv2d_igemm (+ its split-K workspace, sized by c2d_conv2d_igemm_workspace_size)."""
+                 out: Tensor, src_pad: bool = False) -> None:
+    """c2d_conv2d_igemm (+ its split-K workspace, sized by c2d_conv2d_igemm_workspace_size).
+    src_pad: x is the zero-bordered layout [n][h + 2][w + 2][c] (c2d_groupnorm_pad)."""
     d = _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma,
-                   ln_beta, silu_in, bias, act, temb, resid, out)
+                   ln_beta, silu_in, bias, act, temb, resid, out, src_pad)
     wsb = lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
     if wsb:
         ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
@@ -85,7 +89,7 @@ def conv2d_igemm(x: Tensor, weight: Tensor, kpad: int, cout: int, ksize: int, st
 
 @conv2d_igemm.register_fake
 def _(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma, ln_beta,
-      silu_in, bias, act, temb, resid, out):
+      silu_in, bias, act, temb, resid, out, src_pad=False):
     return None
 
 
@@ -124,6 +128,18 @@ def groupnorm(x: Tensor, x2: Optional[Tensor], groups: int, eps: float, gamma: T
     ws = torch.empty((wsb + 15) // 16 * 4, device=x.device, dtype=torch.float32) if wsb else None
     check(lib().c2d_groupnorm(ptr(x), ptr(x2), c0, c1, n, hw, groups, eps, ptr(gamma), ptr(beta), int(silu), ptr(out),
                               ptr(ws), wsb, stream_ptr()), "c2d_groupnorm")
+
+
+@custom_op("c2d::groupnorm_pad", mutates_args=("out",), device_types=_CU)
+def groupnorm_pad(x: Tensor, x2: Optional[Tensor], groups: int, eps: float, gamma: Tensor, beta: Tensor, silu: bool,
+                  out: Tensor) -> None:
+    """c2d_groupnorm_pad: x [n][h][w][c0] (+ x2) -> out [n][h + 2][w + 2][c0 + c1], zero border."""
+    n, h, w, c0 = x.shape
+    c1 = x2.shape[-1] if x2 is not None else 0
+    wsb = lib().c2d_groupnorm_pad_workspace_size(n, c0 + c1, h, w)
+    ws = torch.empty((wsb + 15) // 16 * 4, device=x.device, dtype=torch.float32)
+    check(lib().c2d_groupnorm_pad(ptr(x), ptr(x2), c0, c1, n, h, w, groups, eps, ptr(gamma), ptr(beta), int(silu),
+                                  ptr(out), ptr(ws), wsb, stream_ptr()), "c2d_groupnorm_pad")
 
 
 @custom_op("c2d::layernorm_stats", mutates_args=("stats",), device_types=_CU)
@@ -240,12 +256,13 @@ def add(a: Tensor, b: Tensor, out: Tensor) -> None:
 
 
 # fake (meta) implementations: every op only mutates caller-allocated outputs
-for _op in (pack_weights, groupnorm_stats, groupnorm_apply, groupnorm, layernorm_stats, layernorm, attention_fwd,
+for _op in (pack_weights, groupnorm_stats, groupnorm_apply, groupnorm, groupnorm_pad, layernorm_stats, layernorm, attention_fwd,
             attention_small, window_attention, htsat_mel_patches, patch_merge_gather, row_mean, softmax_rows,
             l2_normalize, clap_log_mel, timestep_embedding, cfg_ddim_step, latent_to_nhwc, upsample_nearest2x, add):
     _op.register_fake(lambda *args, **kwargs: None)
 
-OPS = ("conv2d_igemm", "pack_weights", "groupnorm_stats", "groupnorm_apply", "groupnorm", "layernorm_stats",
+OPS = ("conv2d_igemm", "pack_weights", "groupnorm_stats", "groupnorm_apply", "groupnorm", "groupnorm_pad",
+       "layernorm_stats",
        "layernorm", "attention_fwd", "attention_small", "window_attention", "htsat_mel_patches", "patch_merge_gather",
        "row_mean", "softmax_rows", "l2_normalize", "clap_log_mel", "timestep_embedding", "cfg_ddim_step",
        "latent_to_nhwc", "upsample_nearest2x", "add")

@@ -271,9 +271,15 @@ class ResnetBlock2D(nn.Module):
         temb = None
         if temb_all is not None:
             temb = temb_all[:, self.temb_off:self.temb_off + self.cout]
-        h = self.conv1(self.norm1.apply(x, skip, silu=True), temb=temb)
+        n, hh, ww, _ = x.shape
+        cin = self.cin
+        # act(GroupNorm) in the zero-bordered layout where the conv planner runs the row-ring 3x3
+        # (tile 42: the c3 batch's level-0 convs), the plain layout elsewhere
+        p1 = ops.rowring_conv(n, hh, ww, cin, self.cout)
+        h = self.conv1(self.norm1.apply(x, skip, silu=True, pad=p1), temb=temb, padded=p1)
         res = self.conv_shortcut(x, x2=skip) if self.conv_shortcut is not None else x
-        return self.conv2(self.norm2.apply(h, silu=True), resid=res, out=out)
+        p2 = ops.rowring_conv(n, hh, ww, self.cout, self.cout)
+        return self.conv2(self.norm2.apply(h, silu=True, pad=p2), resid=res, out=out, padded=p2)
 
 
 class Downsample2D(nn.Module):

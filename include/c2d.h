@@ -92,6 +92,9 @@ typedef struct c2d_conv_desc {
     int out_ld;
     void* ws;                /* optional split-K workspace (16-B aligned) or NULL         */
     size_t ws_bytes;         /* its size; below c2d_conv2d_igemm_workspace_size(): no split */
+    int src_pad;             /* 1: src0 is zero-bordered, [n][h+2][w+2][c0] (c2d_groupnorm_pad):
+                                3x3, stride 1, one source, output h x w; tile 42 (the row-ring
+                                conv) runs it at w = 64, every other tile as a valid 3x3     */
 } c2d_conv_desc;
 
 int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
@@ -177,6 +180,19 @@ size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups);
 int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups,
                   float eps, const float* gamma, const float* beta, int silu, void* out,
                   void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * c2d_groupnorm writing the zero-bordered layout out[n][h + 2][w + 2][c0 + c1] (border
+ * pixels 0, interior = act(GroupNorm(cat[src0, src1]))): the input of a 3x3 conv with
+ * c2d_conv_desc::src_pad = 1 (ResnetBlock2D.norm1/norm2 + SiLU feeding conv1/conv2), whose
+ * taps then need no halo masks and which tile 42 (the row-ring conv) stages once per channel
+ * block.  Statistics as c2d_groupnorm_stats (deterministic); ws >=
+ * c2d_groupnorm_pad_workspace_size(n, c0 + c1, h, w) bytes, 16-B aligned.
+ */
+size_t c2d_groupnorm_pad_workspace_size(int n, int c, int h, int w);
+int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int c1, int n, int h, int w, int groups,
+                      float eps, const float* gamma, const float* beta, int silu, void* out, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /*
  * LayerNorm over rows of a row-major fp16 [m][c] matrix (leading dim ld).

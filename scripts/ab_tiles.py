@@ -41,24 +41,32 @@ SHAPES = {
     "geglu0_c2": (1, 64, 320, 2560, "geglu", 2, False),
     "conv0_c2": (3, 64, 320, 320, None, 2, True),
     "geglu0_c5": (1, 96, 320, 2560, "geglu", 8, False),
+    # zero-bordered sources (c2d_groupnorm_pad -> conv(padded=True)): the row-ring tile 42 at 64^2
+    "conv0p": (3, 64, 320, 320, None, 16, True, True),
+    "convt0p": (3, 64, 320, 320, None, 16, False, True),
+    "upconv0p": (3, 64, 960, 320, None, 16, False, True),
+    "conv0_c2p": (3, 64, 320, 320, None, 2, True, True),
 }
 
 
-def make(k, h, cin, cout, act, n, resid, dev):
+def make(k, h, cin, cout, act, n, resid, dev, pad=False):
     g = torch.Generator(device="cpu").manual_seed(0)
     x = torch.randn(n, h, h, cin, generator=g).to(dev, torch.float16)
+    if pad:
+        x = torch.nn.functional.pad(x, (0, 0, 1, 1, 1, 1)).contiguous()
     w = torch.randn(cout, cin, k, k, generator=g) / math.sqrt(k * k * cin)
     wp, kp = ops.pack_conv_weight(w)
     wp = wp.to(dev)
     b = torch.randn(cout, generator=g).to(dev) * 0.1
     r = torch.randn(n, h, h, cout, generator=g).to(dev, torch.float16) if resid else None
     out = torch.empty(n, h, h, cout // 2 if act == "geglu" else cout, device=dev, dtype=torch.float16)
-    return dict(x=x, wp=wp, kp=kp, cout=cout, k=k, b=b, r=r, out=out, act=act,
+    return dict(x=x, wp=wp, kp=kp, cout=cout, k=k, b=b, r=r, out=out, act=act, pad=pad,
                 flop=2.0 * n * h * h * cout * k * k * cin)
 
 
 def call(c):
-    ops.conv(c["x"], c["wp"], c["kp"], c["cout"], ksize=c["k"], bias=c["b"], act=c["act"], resid=c["r"], out=c["out"])
+    ops.conv(c["x"], c["wp"], c["kp"], c["cout"], ksize=c["k"], bias=c["b"], act=c["act"], resid=c["r"], out=c["out"],
+             padded=c["pad"])
 
 
 def main():
@@ -70,7 +78,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda")
     plans = [tuple(int(v) for v in p.split(":")) if ":" in p else (int(p), 0) for p in a.plans.split(",")]
-    cases = {s: make(*SHAPES[s], dev) for s in a.shapes.split(",")}
+    cases = {s: make(*SHAPES[s][:7], dev, *SHAPES[s][7:]) for s in a.shapes.split(",")}
     times = {(s, p): [] for s in cases for p in plans}
     used = {}
     outs = {}

@@ -20,7 +20,7 @@ static int fails = 0;
         }                                                                     \
     } while (0)
 
-static const int kTiles[] = {0, 1, 2, 3, 7, 8, 9, 25, 28, 29, 40, 41, 50};
+static const int kTiles[] = {0, 1, 2, 3, 7, 8, 9, 25, 28, 29, 40, 41, 42, 50};
 
 static c2d_conv_desc desc(int n, int h, int w, int c0, int c1, int ksize, int stride, int cout, int act) {
     static char dummy[64] __attribute__((aligned(16)));
@@ -84,6 +84,22 @@ int main() {
         }
     check_plan(desc(16, 64, 64, 640, 320, 3, 1, 320, C2D_ACT_NONE));   // up-block skip concat
     check_plan(desc(16, 64, 64, 320, 0, 3, 2, 320, C2D_ACT_NONE));     // stride-2 downsample
+    // zero-bordered sources (c2d_groupnorm_pad): the row-ring tile 42 at c3's level 0, planner tiles elsewhere
+    for (int nb : {2, 16})
+        for (int hw : {64, 32, 16})
+            for (int cc : {320, 640, 960}) {
+                c2d_conv_desc d = desc(nb, hw, hw, cc, 0, 3, 1, 320, C2D_ACT_NONE);
+                d.src_pad = 1;
+                check_plan(d);
+                int tile = -1, split = -1;
+                CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK);
+                CHECK((tile == 42) == (nb == 16 && hw == 64));
+            }
+    {
+        c2d_conv_desc d = desc(16, 64, 64, 320, 0, 3, 2, 320, C2D_ACT_NONE);
+        d.src_pad = 1;   // a padded source is stride 1 only
+        CHECK(c2d_conv2d_igemm(&d, nullptr) == C2D_E_SHAPE);
+    }
     for (int nb : {1, 2, 8})                                            // VAE decoder
         for (int hw : {64, 128, 256, 512})
             for (int c : {128, 256, 512}) check_plan(desc(nb, hw, hw, c, 0, 3, 1, c, C2D_ACT_NONE));

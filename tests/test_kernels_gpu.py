@@ -215,6 +215,79 @@ def test_split_k_cancelling_partials_beyond_fp16(dev, force_plan, n, h, cin, cou
     close(nchw(out), ref, tol_max=5e-3, tol_l2=2e-3)
 
 
+@pytest.mark.parametrize("n,h,w,c0,c1,silu", [
+    (2, 16, 24, 320, 0, True),      # non-square, the small-image path's shapes
+    (16, 64, 64, 320, 0, True),     # c3's level-0 norm1 / norm2
+    (2, 64, 64, 640, 320, True),    # an up block's norm1 over the skip concat
+    (3, 8, 8, 1280, 0, False),
+])
+def test_groupnorm_pad(dev, n, h, w, c0, c1, silu):
+    """c2d_groupnorm_pad: act(GroupNorm(cat[x, x2])) written zero-bordered, [n][h+2][w+2][c]."""
+    c = c0 + c1
+    x = gen(n, c, h, w, seed=141, scale=2.0) + 0.3
+    gamma, beta = gen(c, seed=142) * 0.2 + 1, gen(c, seed=143) * 0.2
+    xd = nhwc(x).half()
+    ref = F.group_norm(nchw(xd.float()), 32, gamma, beta, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    ref = F.pad(ref, (1, 1, 1, 1))
+    xd = xd.to(dev)
+    x0, x1 = (xd[..., :c0].contiguous(), xd[..., c0:].contiguous()) if c1 else (xd, None)
+    out = ops.group_norm(x0, 32, 1e-5, gamma.to(dev), beta.to(dev), silu, x2=x1, pad=True)
+    assert out.shape == (n, h + 2, w + 2, c)
+    o = out.float().cpu()
+    border = torch.ones(h + 2, w + 2, dtype=torch.bool)
+    border[1:-1, 1:-1] = False
+    assert (o[:, border] == 0).all(), "border pixels must be exact zeros"
+    close(nchw(o), ref)
+
+
+@pytest.mark.parametrize("n,h,cin,cout,tile,split,form", [
+    (16, 64, 320, 320, 0, 0, "resid"),    # c3's level-0 conv2: the planner's tile 42
+    (16, 64, 640, 320, 0, 0, "temb"),     # an up block's conv1 over the concat (GN'd into one padded source)
+    (4, 64, 320, 320, 42, 1, "plain"),    # forced tile 42 on a 64-tile grid
+    (4, 64, 320, 640, 42, 5, "resid"),    # forced split: one channel block per slice
+    (4, 64, 960, 320, 42, 4, "temb"),     # 15 channel blocks in 4 slices (4, 4, 4, 3)
+    (2, 32, 320, 640, 0, 0, "resid"),     # other tiles over the padded source (a valid 3x3)
+    (2, 16, 1280, 1280, 0, 0, "temb"),
+    (3, 8, 640, 320, 7, 2, "plain"),
+])
+def test_conv3x3_padded_source(dev, force_plan, n, h, cin, cout, tile, split, form):
+    """3x3 conv over a zero-bordered source (c2d_conv_desc::src_pad): the row-ring tile 42
+    (igemm_pp16r.h: 6 padded image rows staged once per channel block, taps as row-shifted
+    fragment reads) and every other tile as a valid 3x3 over the padded image."""
+    x = gen(n, cin, h, h, seed=151)
+    w = gen(cout, cin, 3, 3, seed=152, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=153)
+    ref = F.conv2d(x, w, b, padding=1)
+    temb = resid = None
+    if form == "temb":
+        temb = gen(n, cout, seed=154)
+        ref = ref + temb[:, :, None, None]
+    if form == "resid":
+        resid = gen(n, cout, h, h, seed=155)
+        ref = ref + resid
+    xp = torch.zeros(n, h + 2, h + 2, cin)
+    xp[:, 1:-1, 1:-1] = nhwc(x)
+    if tile:
+        force_plan(tile, split)
+    wp, kp = ops.pack_conv_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(xp.half().to(dev), wp.to(dev), kp, cout, ksize=3, bias=b.float().to(dev), padded=True,
+                       temb=None if temb is None else temb.half().to(dev),
+                       resid=None if resid is None else nhwc(resid).half().to(dev))
+    assert out.shape == (n, h, h, cout)
+    if tile:
+        assert plans == [(tile, split)], plans
+    elif n == 16 and h == 64:
+        assert plans[0][0] == 42, plans
+    else:
+        assert plans[0][0] != 42, plans
+    if not tile:
+        assert ops.rowring_conv(n, h, h, cin, cout) == (n == 16 and h == 64)
+    close(nchw(out), ref)
+
+
 @pytest.mark.parametrize("n,h,w,cin,cout,act,bias", [
     (3, 61, 61, 320, 2560, "geglu", True),    # K = 320 (5 K steps), 590 tiles: several per workgroup, ragged M
     (16, 64, 64, 320, 960, None, False),      # the L0 QKV shape, 342 x 4 tiles, no bias
