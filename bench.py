@@ -40,28 +40,35 @@ def log(*a):
 
 def measure_dominant_kernel(dev, iters: int = 20):
     """The dominant kernel is the implicit-GEMM conv (c2d_conv2d_igemm): time its
-    most frequent heavy launch, the level-0 ResnetBlock2D conv (320 -> 320, 3x3,
-    N = 16 CFG images, 64x64) with HIP events on the stream it is launched on."""
+    most frequent heavy launch, the level-0 ResnetBlock2D conv2 (320 -> 320, 3x3 + residual,
+    N = 16 CFG images, 64x64) as the UNet runs it -- over the zero-bordered GroupNorm output
+    (c2d_groupnorm_pad) on the row-ring tile 42 -- with HIP events on the stream it is
+    launched on."""
     from clap2diffusion_amd import ops
     n, h, c = 16, 64, 320
     x = torch.randn(n, h, h, c, device=dev, dtype=torch.float16)
+    xp = torch.nn.functional.pad(x, (0, 0, 1, 1, 1, 1)).contiguous()   # [n, h + 2, w + 2, c], zero border
     w = torch.randn(c, c, 3, 3, device=dev) / math.sqrt(9 * c)
     wp, kp = ops.pack_conv_weight(w)
     b = torch.zeros(c, device=dev)
     res = torch.randn_like(x)
     out = torch.empty_like(x)
+
+    def call():
+        ops.conv(xp, wp, kp, c, ksize=3, bias=b, resid=res, out=out, padded=True)
     with ops.record_conv_plans() as plans:
-        ops.conv(x, wp, kp, c, ksize=3, bias=b, resid=res, out=out)
+        call()
     for _ in range(2):
-        ops.conv(x, wp, kp, c, ksize=3, bias=b, resid=res, out=out)
+        call()
     tile, split = plans[0]
-    kname = {40: "igemm_pp16_kernel<5,3,4> 256x320 ping-pong 16x16x32, 4 phases per K step",
+    kname = {42: "igemm_pp16r_kernel<5,4> 256x320 row-ring ping-pong 16x16x32 over the zero-bordered source",
+             40: "igemm_pp16_kernel<5,3,4> 256x320 ping-pong 16x16x32, 4 phases per K step",
              25: "igemm_m32_kernel 256x320 32x32x16"}.get(tile, f"tile {tile}")
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(iters):
-        ops.conv(x, wp, kp, c, ksize=3, bias=b, resid=res, out=out)
+        call()
     e1.record(s)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / iters
@@ -69,7 +76,7 @@ def measure_dominant_kernel(dev, iters: int = 20):
     tflops = flop / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / PEAK_F16_TFLOPS, 4), "traffic": None,
-            "kernel": f"c2d_conv2d_igemm ({kname}, split {split}) level-0 ResnetBlock2D conv 3x3 320->320 + "
+            "kernel": f"c2d_conv2d_igemm ({kname}, split {split}) level-0 ResnetBlock2D conv2 3x3 320->320 + "
                       "residual, N=16 (CFG pair x 8 images) x 64x64",
             "flop_per_launch": flop, "avg_us": round(ms * 1e3, 2)}
 
@@ -243,7 +250,8 @@ def main():
         unet_tf = UNET_GFLOP_PER_SAMPLE * (a.res / 512) ** 2 * 2 * a.ddim_steps * total_images / dt / 1e3
         roof["pipeline_unet_tflops"] = round(unet_tf, 2)
         n_, h_, c_ = 16, 64, 320
-        roof["algorithmic_bytes"] = 2 * (3 * n_ * h_ * h_ * c_ + c_ * 9 * c_)  # x + resid + out + weights
+        # padded x + resid + out + weights
+        roof["algorithmic_bytes"] = 2 * (n_ * (h_ + 2) ** 2 * c_ + 2 * n_ * h_ * h_ * c_ + c_ * 9 * c_)
         if not a.no_pmc and ctx.world == 1:
             tr, src = pmc_traffic()
             roof["traffic"] = None if tr is None else round(tr)

@@ -65,8 +65,10 @@ def key(args, kw):
     x2 = kw.get("x2")
     cin = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
     m = x.numel() // x.shape[-1]
+    if kw.get("padded"):   # zero-bordered source [n][h + 2][w + 2][c]: output rows n * h * w
+        m = x.shape[0] * (x.shape[1] - 2) * (x.shape[2] - 2)
     return (kw["ksize"], m, cin, cout, kw.get("stride", 1), bool(kw.get("up")), kw.get("act"),
-            kw.get("resid") is not None, kw.get("temb") is not None)
+            kw.get("resid") is not None, kw.get("temb") is not None, bool(kw.get("padded")))
 
 
 groups = collections.OrderedDict()
@@ -88,7 +90,7 @@ for k, lst in groups.items():
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
-    ks, m, cin, cout, st, up, act, res, temb = k
+    ks, m, cin, cout, st, up, act, res, temb, pad = k
     oh_m = m if ks == 1 else m // (st * st) * (4 if up else 1)
     fl = 2.0 * oh_m * cout * ks * ks * cin
     rows.append((k, len(lst), plans[0] if plans else None, us, fl))
@@ -96,7 +98,7 @@ for k, lst in groups.items():
 tot = sum(c * us for _, c, _, us, _ in rows)
 print(f"total {tot / 1e3:.2f} ms per UNet call in conv / GEMM")
 for k, c, pl, us, fl in sorted(rows, key=lambda r: -r[1] * r[3]):
-    ks, m, cin, cout, st, up, act, res, temb = k
+    ks, m, cin, cout, st, up, act, res, temb, pad = k
     tag = f"{'3x3' if ks == 3 else '1x1'} M={m:6d} {cin:4d}->{cout:5d}" + (f" s{st}" if st > 1 else "") + \
-          (" up" if up else "") + (f" {act}" if act else "") + (" +res" if res else "") + (" +temb" if temb else "")
+          (" up" if up else "") + (" pad" if pad else "") + (f" {act}" if act else "") + (" +res" if res else "") + (" +temb" if temb else "")
     print(f"{tag:48s} x{c:2d} plan={pl} {us:8.1f} us {fl / us / 1e6:7.1f} TF/s  {100 * c * us / tot:5.1f}%", flush=True)
