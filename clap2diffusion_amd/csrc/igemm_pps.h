@@ -23,12 +23,16 @@
 // flushed after the loop.  Plain outputs without a residual / time embedding only.
 #pragma once
 
+#ifndef C2D_PPS_AUX
+#define C2D_PPS_AUX 0   // cache policy of the carried-epilogue stores (A/B builds: 2 = nt, 16 = sc1)
+#endif
+
 namespace c2d {
 
 template <int NK, bool GG, int PH>
 __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
     constexpr int TN = 4, TMW = 6, BK = 64, NW = 8;
-    constexpr int BM = 2 * TMW * 16, BN = 4 * TN * 16;   // 192 x 256
+    constexpr int BM = 2 * TMW * 16, BN = 4 * TN * 16;   // 192 x 256 (a 256-row tile: 256 VGPRs + 66-129 spilled)
     constexpr int RB = 2 * BK, STAGE = (BM + BN) * RB;
     typedef M32Loader<BM, BN, BK, NW, 1> Loader;
     constexpr int P = Loader::PMAX, SA = Loader::SA, SB = Loader::SB;
@@ -37,7 +41,7 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
     // 24-MFMA sections (half the barriers, all six A row tiles' fragments live; every DMA piece
     // of the next K step dealt in phase 0).  L0 GEGLU (K = 320) same box, three alternations:
     // 172.3-173.7 us with 4 phases, 165.1-166.7 with 2; K = 640 / 1280 keep 4 (2 spills 34 VGPRs)
-    constexpr int RT = PH == 4 ? 3 : 6;
+    constexpr int RT = PH == 4 ? TMW / 2 : TMW;
     static_assert(PH == 2 || PH == 4, "pps phases per K step");
     constexpr int PPH = (P + PH - 2) / (PH - 1);   // pieces per phase, phases 0..PH-2
     constexpr int NSEC = PH * NK;        // sections (phases) per tile
@@ -113,7 +117,7 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
             asm volatile("" :: "v"(o), "v"(off));
             return;
         }
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ro, (int)off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ro, (int)off, 0, C2D_PPS_AUX);
     };
 
     f32x4 acc[TN][TMW];
@@ -158,7 +162,7 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
                 }
 #pragma unroll
                 for (int t = 0; t < RT; ++t)
-                    fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + (rh * 3 + t) * 16 * RB + fo);
+                    fa[t] = *reinterpret_cast<const f16x8*>(S + a_base + (rh * RT + t) * 16 * RB + fo);
                 if (q < PH - 1 && nxt) {
 #pragma unroll
                     for (int i = 0; i < PPH; ++i)
@@ -173,8 +177,8 @@ __global__ void __launch_bounds__(512) igemm_pps_kernel(IgemmParams p) {
                 for (int b = 0; b < RT; ++b)
 #pragma unroll
                     for (int a = 0; a < TN; ++a)
-                        acc[a][rh * 3 + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                            fb[a], fa[b], (kt == 0 && ks == 0) ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[a][rh * 3 + b],
+                        acc[a][rh * RT + b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                            fb[a], fa[b], (kt == 0 && ks == 0) ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[a][rh * RT + b],
                             0, 0, 0);
                 static_for<(sec * NU) / NSEC, ((sec + 1) * NU) / NSEC>(unit);
                 __builtin_amdgcn_s_setprio(0);

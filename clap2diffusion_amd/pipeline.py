@@ -22,7 +22,6 @@ from __future__ import annotations
 import argparse
 import os
 import warnings
-import wave
 from pathlib import Path
 
 import numpy as np
@@ -62,16 +61,55 @@ def initial_latents(seeds: list[int], h: int, w: int, device=None) -> torch.Tens
     return torch.stack(lat).to(device)
 
 
-def _read_wav(path: str) -> tuple[np.ndarray, int]:
-    with wave.open(str(path), "rb") as f:
-        sr, ch, sw, n = f.getframerate(), f.getnchannels(), f.getsampwidth(), f.getnframes()
-        raw = f.readframes(n)
-    dt = {1: np.uint8, 2: np.int16, 4: np.int32}[sw]
-    x = np.frombuffer(raw, dtype=dt).astype(np.float32)
-    if sw == 1:
-        x = (x - 128.0) / 128.0
+_WAVE_PCM, _WAVE_FLOAT, _WAVE_EXTENSIBLE = 1, 3, 0xFFFE
+
+
+def _read_wav(path: str, max_seconds: float | None = None) -> tuple[np.ndarray, int]:
+    """RIFF/WAVE reader -> (mono float32 in [-1, 1], native rate): PCM 8 (unsigned) / 16 / 24 / 32-bit,
+    IEEE float 32 / 64-bit, WAVE_FORMAT_EXTENSIBLE of either; channels averaged (librosa mono=True).
+    max_seconds: keep the first max_seconds of the file at its native rate (librosa's duration=,
+    applied before resampling as librosa.load does).  Other containers (mp3, flac, ...) need a
+    decoder this image does not have: convert them to WAV first."""
+    data = Path(path).read_bytes()
+    if data[:4] != b"RIFF" or data[8:12] != b"WAVE":
+        raise ValueError(f"{path}: not a RIFF/WAVE file (only WAV is decoded without librosa)")
+    fmt = None
+    pos = 12
+    body = None
+    while pos + 8 <= len(data):
+        cid, size = data[pos:pos + 4], int.from_bytes(data[pos + 4:pos + 8], "little")
+        chunk = data[pos + 8:pos + 8 + size]
+        if cid == b"fmt ":
+            tag, ch, sr = int.from_bytes(chunk[0:2], "little"), int.from_bytes(chunk[2:4], "little"), \
+                int.from_bytes(chunk[4:8], "little")
+            bits = int.from_bytes(chunk[14:16], "little")
+            if tag == _WAVE_EXTENSIBLE and len(chunk) >= 26:
+                tag = int.from_bytes(chunk[24:26], "little")   # first two bytes of the SubFormat GUID
+            fmt = (tag, ch, sr, bits)
+        elif cid == b"data":
+            body = chunk
+        pos += 8 + size + (size & 1)
+    if fmt is None or body is None:
+        raise ValueError(f"{path}: WAV without fmt / data chunk")
+    tag, ch, sr, bits = fmt
+    bps = bits // 8
+    frames = len(body) // (bps * ch)
+    if max_seconds is not None:
+        frames = min(frames, int(max_seconds * sr))
+    body = body[: frames * bps * ch]
+    if tag == _WAVE_FLOAT and bits in (32, 64):
+        x = np.frombuffer(body, dtype=np.float32 if bits == 32 else np.float64).astype(np.float32)
+    elif tag == _WAVE_PCM and bits == 8:
+        x = (np.frombuffer(body, dtype=np.uint8).astype(np.float32) - 128.0) / 128.0
+    elif tag == _WAVE_PCM and bits in (16, 32):
+        x = np.frombuffer(body, dtype=np.int16 if bits == 16 else np.int32).astype(np.float32) / float(2 ** (bits - 1))
+    elif tag == _WAVE_PCM and bits == 24:
+        b = np.frombuffer(body, dtype=np.uint8).reshape(-1, 3).astype(np.int32)
+        v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        x = v.astype(np.float32) / float(1 << 23)
     else:
-        x /= float(2 ** (8 * sw - 1))
+        raise ValueError(f"{path}: unsupported WAV encoding (format tag {tag}, {bits} bits)")
     return x.reshape(-1, ch).mean(axis=1), sr
 
 
@@ -164,7 +202,7 @@ class AudioToImageInference:
         if str(audio_path).startswith("synthetic:"):
             audio = synthetic_thunder(int(str(audio_path).split(":", 1)[1] or 0), duration)
         else:
-            x, sr = _read_wav(audio_path)
+            x, sr = _read_wav(audio_path, max_seconds=duration)
             if sr != SR:
                 from scipy.signal import resample_poly
                 g = np.gcd(sr, SR)

@@ -17,6 +17,7 @@ for name in ${NAMES:-geglu0 qkv0 res0 l2res}; do
     res0) ARGS="1 64 320 320 6 --res" ;;
     l2res) ARGS="1 16 1280 1280 6 --res" ;;
     conv0) ARGS="3 64 320 320 6 --res" ;;
+    conv0p) ARGS="3 64 320 320 6 --res --pad" ;;
   esac
   timeout -s KILL 90 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/kt_$name -o k -- python3 -u scripts/one_gemm.py $ARGS > $D/${name}_kt.log 2>&1 || { echo "$name kt failed"; tail -5 $D/${name}_kt.log; exit 1; }
   cp $(find /tmp/kt_$name -name "*kernel_stats.csv" | head -1) $D/${name}_kernel_stats.csv
