@@ -933,6 +933,7 @@ static const PlanHint kPlanHints[] = {
     {3, 8192, 5760, 320, false, 40, 6},       // 3x3 L0 640 -> 320: 58.2 -> 54.7
     {3, 8192, 8640, 320, false, 40, 8},       // 3x3 L0 960 -> 320: 72.8 -> 66.9
     {3, 2048, 5760, 640, false, 7, 8},        // 3x3 L1 640: 42.3 -> 38.7
+    {3, 2048, 17280, 640, false, 40, 16},     // 3x3 L1 1920 -> 640: 73.4 -> 67.0 (r04 fp32 slabs)
     {3, 512, 11520, 1280, false, 7, 12},      // 3x3 L2 1280: 55.2 -> 43.7 (split 12)
     {3, 512, 17280, 1280, false, 41, 16},     // 3x3 L2 1920 -> 1280: 75.2 -> 48.3
     {3, 512, 23040, 1280, false, 41, 16},     // 3x3 L2 2560 -> 1280: 95.4 -> 57.1
@@ -955,7 +956,8 @@ static const PlanHint kPlanHints[] = {
     // N = 16, 64^2 (c3)
     {1, 4096, 1280, 1280, false, 8, 1},       // 1x1 L2: 27.2 -> 24.5
     {1, 1024, 1280, 1280, false, 3, 1},       // 1x1 mid: 18.9 -> 13.5
-    {3, 1024, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 97.2 -> 91.3
+    {3, 1024, 11520, 1280, false, 41, 12},    // 3x3 L3 1280: 61.2 -> 52.5 (r04 re-sweep, fp32 slabs)
+    {3, 1024, 23040, 1280, false, 41, 12},    // 3x3 L3 2560 -> 1280: 97.2 -> 91.3 (split 8); 87.9 -> 77.3 (r04: 12)
     {1, 4096, 6400, 1280, false, 7, 2},       // ff.net.2 + proj_out fold L2: 84.7 -> 82.2
     // VAE decoder at batch 8 (profiles/r03_sweep_vae.txt): only the 1x1 shortcuts gain
     {1, 2097152, 256, 128, false, 1, 1},      // 512^2 256 -> 128: 511.9 -> 459.4

@@ -9,4 +9,4 @@ timeout -k 10 400 python -u scripts/sweep_tiles_graph.py --batch 8 --only "L2" -
 timeout -k 10 400 python -u scripts/sweep_tiles_graph.py --batch 8 --only "L3" --splits 1,2,4,6,8,12,16 > $O/sweep_b8_l3.txt 2>&1 || { tail -5 $O/sweep_b8_l3.txt; exit 1; }
 timeout -k 10 400 python -u scripts/sweep_tiles_graph.py --batch 8 --only "L1 3x3" --splits 1,2,3,4 > $O/sweep_b8_l1.txt 2>&1 || { tail -5 $O/sweep_b8_l1.txt; exit 1; }
 timeout -k 10 500 python -u scripts/sweep_tiles_graph.py --batch 1 --only "3x3" --splits 1,2,4,6,8,12,16 > $O/sweep_b1_3x3.txt 2>&1 || { tail -5 $O/sweep_b1_3x3.txt; exit 1; }
-grep -v amdgpu.ids $O/sweep_*.txt | grep -v "^ " | head -200
+echo sweeps done
