@@ -21,6 +21,8 @@ def _ks(n):
 
 
 def family(n):
+    if "igemm_pp16r_kernel" in n:   # the row-ring tile is 3x3-only (its template has no KS argument)
+        return "conv3x3"
     if "igemm_" in n and "<" in n and "igemm_kernel" not in n:
         return "conv3x3" if _ks(n) == "3" else "gemm1x1"
     for key, f in (("igemm_kernel", "gemm_reg"), ("splitk", "splitk"), ("attn_fwd", "attention"), ("attn_small", "attention"),
