@@ -1,7 +1,7 @@
 """End-to-end fp32 CPU reference of the sampling path (TEST ORACLE ONLY):
-waveform -> preprocess + log-mel (mel_ref) -> HTSAT (htsat_ref) ->
-ImprovedHierarchicalAudioEncoder (the API-kept torch module, pinned by
-tests/golden/projectors.npz) -> CLIP text tower (transformers CLIPTextModel,
+waveform -> preprocess + log-mel (mel_ref) -> HTSAT (htsat_ref) -> the projectors' routed
+tokens (projectors_ref: plain tensor functions, pinned by tests/golden/projectors.npz; the
+product's projector modules are not used here) -> CLIP text tower (transformers CLIPTextModel,
 clip_ref) -> UNetRef + DDIM/CFG (ddim_ref) -> VAEDecoderRef, on the same seeded
 weights as clap2diffusion_amd.pipeline.AudioToImageInference(seed).
 
@@ -15,11 +15,11 @@ import numpy as np
 import torch
 
 from clap2diffusion_amd import weights as W
-from clap2diffusion_amd.projectors import ImprovedHierarchicalAudioEncoder
 from oracle.clip_ref import clip_text_model
 from oracle.ddim_ref import alphas_cumprod, ddim_step, timesteps
 from oracle.htsat_ref import htsat_forward
 from oracle.mel_ref import log_mel
+from oracle.projectors_ref import projector_shapes, routed_tokens
 from oracle.unet_ref import UNetRef
 from oracle.vae_ref import VAEDecoderRef
 
@@ -30,7 +30,9 @@ class ReferencePipeline:
     def __init__(self, seed: int = 0):
         self.seed = seed
         self.htsat_sd = W.synth_htsat(seed)
-        self.enc = W.fill_module(ImprovedHierarchicalAudioEncoder(), "improved.", seed).eval()
+        # the product's seeded recipe, key by key (W.synth_generic seeds every tensor from its name):
+        # the same projector weights as pipeline.AudioToImageInference(seed), without its modules
+        self.enc_sd = W.synth_generic(projector_shapes(), seed, "improved.")
         self.clip = clip_text_model(seed)
         procs = {lv: W.synth_processor_weights(lv, seed) for lv in ("early", "mid", "late")}
         self.unet = UNetRef(W.synth_unet(seed), processors=procs)
@@ -44,8 +46,7 @@ class ReferencePipeline:
     @torch.no_grad()
     def condition(self, mel: torch.Tensor, ids_uncond: torch.Tensor, ids_cond: torch.Tensor):
         clap = htsat_forward(self.htsat_sd, mel[:, None].float())
-        _, info = self.enc(clap, return_all=True)
-        audio = {k: torch.cat([v, v], 0) for k, v in info["routed"].items()}
+        audio = {k: torch.cat([v, v], 0) for k, v in routed_tokens(clap, self.enc_sd)["routed"].items()}
         ehs = self.clip(input_ids=torch.cat([ids_uncond, ids_cond], 0).cpu()).last_hidden_state.float()
         return ehs, audio
 

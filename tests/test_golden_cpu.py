@@ -57,6 +57,22 @@ def test_projectors_match_reference():
         assert torch.allclose(got, ref, atol=2e-5, rtol=1e-4), (key, (got - ref).abs().max().item())
 
 
+def test_oracle_projector_matches_golden():
+    """oracle/projectors_ref (plain tensor functions, no product module) against the
+    reference-module goldens: the routed tokens the end-to-end oracle feeds its UNet."""
+    from clap2diffusion_amd.weights import synth_generic
+    from oracle.projectors_ref import projector_shapes, routed_tokens
+    gd = np.load(G / "projectors.npz")
+    sd = synth_generic(projector_shapes(), 0, "improved.")
+    got = routed_tokens(torch.from_numpy(gd["clap"]), sd)
+    pairs = [(got["tokens_10"], "tokens_10"), (got["assignments"], "assignments"),
+             (got["hierarchy_weights"], "hierarchy_weights")] + \
+            [(got["routed"][lv], "routed_" + lv) for lv in ("early", "mid", "late")]
+    for t, key in pairs:
+        ref = torch.from_numpy(gd[key])
+        assert torch.allclose(t, ref, atol=2e-5, rtol=1e-4), (key, (t - ref).abs().max().item())
+
+
 def test_projector_state_dict_keys_match_reference_layout():
     enc = P.ImprovedHierarchicalAudioEncoder()
     keys = set(enc.state_dict())
