@@ -211,6 +211,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-configs", action="store_true", help="skip the c1/c2/c5 side measurements")
+    ap.add_argument("--dtype", default="fp16", choices=["fp16"],
+                    help="compute dtype of the HIP path (fp16 storage, fp32 accumulation; the only one built)")
     a = ap.parse_args()
 
     from clap2diffusion_amd import distributed as D
@@ -268,7 +270,7 @@ def main():
             "metric": "512x512 images/sec @ 50 DDIM steps, batch=8, 1/2/4/8 MI355X",
             "value": round(value, 4), "unit": "images/sec", "n_gpus": ctx.world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic (seeded thunder-like audio, fixed token ids, random-init SD1.5/CLAP weights)",
             "config": {"workload": f"{cfg_name}: batch={B}/GPU, {a.ddim_steps} DDIM steps, {a.res}x{a.res}, CFG 7.5, "
                                    "log-mel+HTSAT+projectors+CLIP+UNet+VAE, all-gather of images",
