@@ -48,10 +48,10 @@ def _digest(defines=()) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(unit, build_dir: Path, defines=()) -> Path:
+def _compile(unit, build_dir: Path, defines=(), flags=()) -> Path:
     src, udefs, stem = unit
     obj = build_dir / (stem + ".o")
-    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in (*defines, *udefs)], *EXTRA.get(src, []), "-c", str(CSRC / src),
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in (*defines, *udefs)], *EXTRA.get(src, []), *flags, "-c", str(CSRC / src),
            "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -60,16 +60,18 @@ def _compile(unit, build_dir: Path, defines=()) -> Path:
 
 
 def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bool = False,
-          variant: str = "", variant_defines: tuple = ()) -> Path:
+          variant: str = "", variant_defines: tuple = (), variant_flags: tuple = ()) -> Path:
     """ablation=True builds libc2d_hip_abl.so with -DC2D_ENABLE_ABLATION (timing-ablation
     switches live; wrong results by design) for scripts/gpu_gemm_abl.sh via C2D_LIB; the
     production libc2d_hip.so never contains them.  variant="x" with variant_defines builds
     libc2d_hip_x.so (compile-time A/B candidates, loaded through C2D_LIB)."""
     defines = ("C2D_ENABLE_ABLATION",) if ablation else tuple(variant_defines)
+    if variant_flags and not variant:
+        raise ValueError("extra compiler flags only for a named A/B variant")
     stem = "libc2d_hip_abl" if ablation else (f"libc2d_hip_{variant}" if variant else "libc2d_hip")
     lib_path = PKG / f"{stem}.so"
     stamp = PKG / f".{stem}.stamp"
-    dig = _digest(defines)
+    dig = _digest(defines + tuple(variant_flags))
     if lib_path.exists() and stamp.exists() and stamp.read_text().strip() == dig and not force:
         if verbose:
             print(f"[c2d] {lib_path.name} up to date ({dig})")
@@ -77,7 +79,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bo
     build_dir = ROOT / "build" / ("c2d_abl" if ablation else (f"c2d_{variant}" if variant else "c2d"))
     build_dir.mkdir(parents=True, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda u: _compile(u, build_dir, defines), UNITS))
+        objs = list(ex.map(lambda u: _compile(u, build_dir, defines, variant_flags), UNITS))
     tmp = lib_path.with_suffix(".so.tmp")
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -104,6 +106,8 @@ if __name__ == "__main__":
     ap.add_argument("--ablation", action="store_true", help="build libc2d_hip_abl.so (timing ablations)")
     ap.add_argument("--variant", default="", help="build libc2d_hip_<variant>.so with --define D ...")
     ap.add_argument("--define", action="append", default=[])
+    ap.add_argument("--cflag", action="append", default=[], help="extra hipcc flag (variant builds only)")
     a = ap.parse_args()
-    build(force=a.force, jobs=a.jobs, ablation=a.ablation, variant=a.variant, variant_defines=tuple(a.define))
+    build(force=a.force, jobs=a.jobs, ablation=a.ablation, variant=a.variant, variant_defines=tuple(a.define),
+          variant_flags=tuple(a.cflag))
     sys.exit(0)
