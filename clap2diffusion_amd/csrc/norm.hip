@@ -388,284 +388,6 @@ __global__ void __launch_bounds__(NT) gn_fused_kernel(const f16* __restrict__ s0
     }
 }
 
-// ---------------------------------------------------------------- single-launch GroupNorm
-// Statistics, fold and apply in ONE launch (replaces partial + finalize + apply: at c2's
-// N = 2 those are three latency-bound launches of 8 + 5 + 6 us per norm).  Grid (P, n): the P
-// workgroups of image n
-//   1. accumulate shifted per-channel moments over their pixel rows (gn_partial_kernel's
-//      per-thread order), total them per channel in LDS, fold each group's channels in a
-//      fixed order and publish one {sum, sumsq} fp32 pair per group as an 8-B agent-scope
-//      (write-through) store;
-//   2. meet at image n's barrier (cdna_hip_programming.md Guideline 16, R1 with a counter):
-//      every storing wave drains its stores, the workgroup syncs, lane 0 adds to the image's
-//      arrival counter; the last arriver bumps the image's generation word, the others poll it
-//      relaxed with s_sleep, bounded.  No acquire fence: every load of the published pairs is
-//      an agent-scope load;
-//   3. fold the P pairs of every group in a fixed order (fp64) -> mean / rstd -> the
-//      per-channel affine of gn_finalize_kernel, redundantly in every workgroup;
-//   4. apply act(x * scale + shift) to their own rows (L2-warm: phase 1 just read them), or in
-//      PAD form to their share of the zero-bordered layout.
-// Deterministic (fixed fold order, independent of arrival order).  Needs all P * n workgroups
-// resident at once: the host sizes P from the occupancy x CU count and otherwise runs the
-// three-launch path.  ws starts with the barrier words, zeroed by a memset node every call;
-// a poll that runs out (never expected) counts in word 0 and poisons that workgroup's output
-// with NaN instead of hanging.
-constexpr int kGnSyncHead = 4;           // u32 words before the per-image {count, generation}
-constexpr unsigned kGnSpinMax = 1u << 17;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-
-// dynamic LDS (floats) of gn_grid_kernel: CPT 1 row-thread moments [R][cin][2] (R * cin <= 2048),
-// channel totals [cin][2], fp64 fold partials [256][2], group mean / rstd [groups][2], 4 flags
-__host__ __device__ inline int gn_grid_lds_floats(int cpt, int cin, int groups) {
-    return (cpt == 1 ? 4096 : 0) + cin * 2 + 1024 + groups * 2 + 4;
-}
-
-__global__ void __launch_bounds__(64) gn_zero_kernel(unsigned* w, int nw) {
-    for (int i = threadIdx.x; i < nw; i += 64) w[i] = 0u;
-}
-
-template <int CPT, bool PAD>
-__global__ void __launch_bounds__(256) gn_grid_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1, int c0,
-                                                      int c1, int hw, int pw, int cpg, int rows_per_block, float eps,
-                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                      int silu, f16* __restrict__ out, unsigned* sync, float* part) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int cin = c0 + c1, nch = cin >> 3, groups = cin / cpg;
-    const int n = blockIdx.y, blk = blockIdx.x, P = gridDim.x;
-    const int t = threadIdx.x;
-    const int R = (CPT == 1) ? 256 / nch : 1;
-    const int ch_base = (CPT == 1) ? (t % nch) : t;
-    const int r0 = (CPT == 1) ? (t / nch) : 0;
-    const bool active = (CPT == 1) ? (t < R * nch) : true;
-    const size_t img = (size_t)n * hw;
-    const int p_begin = blk * rows_per_block;
-    const int p_end = min(hw, p_begin + rows_per_block);
-    float* red = lds;                                              // CPT 1: [R][cin][2]
-    float* chs = lds + (CPT == 1 ? 4096 : 0);                      // [cin][2]
-    double* dacc = reinterpret_cast<double*>(chs + cin * 2);       // [256][2]
-    float* gmr = reinterpret_cast<float*>(dacc + 512);             // [groups][2]: mean, rstd
-    int* flag = reinterpret_cast<int*>(gmr + groups * 2);
-
-    // ---- 1. per-thread shifted moments (gn_partial_kernel's loop and order)
-    float sum[CPT][8], sq[CPT][8], shift[CPT][8];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { sum[q][i] = 0.f; sq[q][i] = 0.f; shift[q][i] = 0.f; }
-    auto ld8 = [&](int pix, int q) {
-        const size_t gp = img + pix;
-        const int c = (ch_base + q * 256) * 8;
-        const f16* ptr = (c < c0) ? (s0 + gp * c0 + c) : (s1 + gp * c1 + (c - c0));
-        return *reinterpret_cast<const f16x8*>(ptr);
-    };
-    if (active) {
-        auto acc8 = [&](const f16x8& v, int q) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                float d = (float)v[i] - shift[q][i];
-                sum[q][i] += d;
-                sq[q][i] += d * d;
-            }
-        };
-        auto load_shift = [&] {
-#pragma unroll
-            for (int q = 0; q < CPT; ++q) {
-                const int ch = ch_base + q * 256;
-                if (ch >= nch) continue;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) shift[q][i] = gn_read(s0, s1, c0, c1, img, ((ch * 8 + i) / cpg) * cpg);
-            }
-        };
-        constexpr int UN = CPT == 1 ? 8 : 4;
-        int pix = p_begin + r0;
-        bool first = true;
-        for (; pix + (UN - 1) * R < p_end; pix += UN * R) {
-            f16x8 v[UN][CPT];
-#pragma unroll
-            for (int u = 0; u < UN; ++u)
-#pragma unroll
-                for (int q = 0; q < CPT; ++q)
-                    if (q == 0 || ch_base + q * 256 < nch) v[u][q] = ld8(pix + u * R, q);
-            if (first) {
-                load_shift();
-                first = false;
-            }
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int u = 0; u < UN; ++u)
-#pragma unroll
-                for (int q = 0; q < CPT; ++q)
-                    if (q == 0 || ch_base + q * 256 < nch) acc8(v[u][q], q);
-        }
-        if (first) load_shift();
-        for (; pix < p_end; pix += R) {
-#pragma unroll
-            for (int q = 0; q < CPT; ++q)
-                if (q == 0 || ch_base + q * 256 < nch) acc8(ld8(pix, q), q);
-        }
-    }
-    // block totals per channel (fixed row order), then per group (fixed channel order)
-    if (CPT == 1) {
-        if (active) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                red[(r0 * cin + ch_base * 8 + i) * 2 + 0] = sum[0][i];
-                red[(r0 * cin + ch_base * 8 + i) * 2 + 1] = sq[0][i];
-            }
-        }
-        __syncthreads();
-        for (int c = t; c < cin; c += 256) {
-            float a = 0.f, b = 0.f;
-            for (int r = 0; r < R; ++r) { a += red[(r * cin + c) * 2]; b += red[(r * cin + c) * 2 + 1]; }
-            chs[c * 2] = a;
-            chs[c * 2 + 1] = b;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < CPT; ++q) {
-            const int ch = ch_base + q * 256;
-            if (ch >= nch) continue;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { chs[(ch * 8 + i) * 2] = sum[q][i]; chs[(ch * 8 + i) * 2 + 1] = sq[q][i]; }
-        }
-    }
-    __syncthreads();
-    gu64* gpart = (gu64*)(part + (size_t)n * P * groups * 2);   // [P][groups] {sum, sumsq} pairs of image n
-    for (int g = t; g < groups; g += 256) {
-        float a = 0.f, b = 0.f;
-        for (int i = 0; i < cpg; ++i) { a += chs[(g * cpg + i) * 2]; b += chs[(g * cpg + i) * 2 + 1]; }
-        const unsigned long long v = ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a);
-        __hip_atomic_store(gpart + (size_t)blk * groups + g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-
-    // ---- 2. image n's barrier
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its pairs
-    __syncthreads();
-    if (t == 0) {
-        gu32* cnt = (gu32*)(sync + kGnSyncHead + 2 * n);
-        gu32* gen = cnt + 1;
-        const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // generation read before this arrival
-        int bad = 0;
-        if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)P - 1) {
-            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // count back at 0 before the release
-            __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            unsigned spins = 0;
-            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
-                if (++spins > kGnSpinMax) {
-                    bad = 1;
-                    __hip_atomic_fetch_add((gu32*)sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        flag[0] = bad;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: loads stay below the poll
-
-    // ---- 3. fixed-order fold of the P pairs per group (fp64), then mean / rstd
-    const int parts = 256 / groups;
-    if (t < parts * groups) {
-        const int g = t % groups, pt = t / groups;
-        double a = 0.0, b = 0.0;
-        int k = pt;
-        for (; k + 3 * parts < P; k += 4 * parts) {
-            unsigned long long v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                v[u] = __hip_atomic_load(gpart + (size_t)(k + u * parts) * groups + g, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                a += (double)__uint_as_float((unsigned)v[u]);
-                b += (double)__uint_as_float((unsigned)(v[u] >> 32));
-            }
-        }
-        for (; k < P; k += parts) {
-            const unsigned long long v =
-                __hip_atomic_load(gpart + (size_t)k * groups + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            a += (double)__uint_as_float((unsigned)v);
-            b += (double)__uint_as_float((unsigned)(v >> 32));
-        }
-        dacc[t * 2] = a;
-        dacc[t * 2 + 1] = b;
-    }
-    __syncthreads();
-    if (t < groups) {
-        double a = 0.0, b = 0.0;
-        for (int pt = 0; pt < parts; ++pt) { a += dacc[(pt * groups + t) * 2]; b += dacc[(pt * groups + t) * 2 + 1]; }
-        const double cntv = (double)hw * cpg;
-        const double m1 = a / cntv;
-        double var = b / cntv - m1 * m1;
-        if (var < 0.0) var = 0.0;
-        const float sft = gn_read(s0, s1, c0, c1, img, t * cpg);
-        gmr[t * 2] = (float)(sft + m1);
-        gmr[t * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
-    }
-    __syncthreads();
-
-    // ---- 4. apply with gn_finalize_kernel's affine
-    const bool bad = flag[0] != 0;
-    float av[CPT][8], bv[CPT][8];
-    bool on[CPT];
-    int cc[CPT];
-#pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-        const int ch = ch_base + q * 256;
-        on[q] = active && ch < nch;
-        cc[q] = (on[q] ? ch : 0) * 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int c = cc[q] + i, gl = c / cpg;
-            const float sc = gamma[c] * gmr[gl * 2 + 1];
-            av[q][i] = bad ? __builtin_nanf("") : sc;
-            bv[q][i] = beta[c] - gmr[gl * 2] * sc;
-        }
-    }
-    auto act8 = [&](const f16x8& v, int q) {
-        f16x8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float y = fmaf((float)v[j], av[q][j], bv[q][j]);
-            if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
-            o[j] = (f16)y;
-        }
-        return o;
-    };
-    if constexpr (PAD) {
-        const int w = pw - 2, ph = hw / w + 2, npix = ph * pw;
-        const int ppb = (npix + P - 1) / P;
-        const int pp_end = min(npix, (blk + 1) * ppb);
-        const size_t pimg = (size_t)n * npix;
-#pragma unroll 2
-        for (int pp = blk * ppb + r0; pp < pp_end; pp += R) {
-            const int py = pp / pw, px = pp - py * pw;
-            const bool inner = py >= 1 && py < ph - 1 && px >= 1 && px < pw - 1;
-            const int pix = inner ? (py - 1) * w + (px - 1) : 0;
-#pragma unroll
-            for (int q = 0; q < CPT; ++q) {
-                if (!on[q]) continue;
-                const f16x8 o = inner ? act8(ld8(pix, q), q) : (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
-                *reinterpret_cast<f16x8*>(out + (pimg + pp) * cin + cc[q]) = o;
-            }
-        }
-        return;
-    }
-#pragma unroll 4
-    for (int pix = p_begin + r0; pix < p_end; pix += R) {
-#pragma unroll
-        for (int q = 0; q < CPT; ++q) {
-            if (!on[q]) continue;
-            *reinterpret_cast<f16x8*>(out + (img + pix) * cin + cc[q]) = act8(ld8(pix, q), q);
-        }
-    }
-}
-
 // ---------------------------------------------------------------- LayerNorm
 // one wave per row, up to 4 chunks (32 values) per lane in registers: exact
 // two-pass mean / variance.
@@ -958,104 +680,14 @@ static int gn_fused_cb(int n, int cin, int groups) {
 static int gn_fused_max_hw() { return tuning().gn_fused_hw; }
 
 static bool gn_use_fused(int n, int cin, int hw, int groups) {
-    return gn_fused_cb(n, cin, groups) > 0 && hw <= gn_fused_max_hw() && tuning().gn_grid < 2;
-}
-
-// workgroups of gn_grid_kernel the device holds at once: CUs x min(2, occupancy of every
-// instantiation at its largest LDS request), once per device.  The in-launch barrier needs
-// the whole grid resident; plans stay within this.
-static int gn_grid_cap() {
-    static std::once_flag once[kMaxDevices];
-    static int cap[kMaxDevices];
-    const int dev = current_device();
-    std::call_once(once[dev], [dev] {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
-            cap[dev] = 0;
-            return;
-        }
-        const size_t lds = (size_t)gn_grid_lds_floats(1, 2048, 256) * sizeof(float);   // >= every CPT 2 request too
-        int occ = 2;
-        const void* ks[4] = {(const void*)gn_grid_kernel<1, false>, (const void*)gn_grid_kernel<2, false>,
-                             (const void*)gn_grid_kernel<1, true>, (const void*)gn_grid_kernel<2, true>};
-        for (const void* k : ks) {
-            int o = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, 256, lds) != hipSuccess) o = 0;
-            if (o < occ) occ = o;
-        }
-        (void)hipGetLastError();
-        cap[dev] = cus * occ;
-    });
-    return cap[dev];
-}
-
-struct GnGridPlan {
-    int cpt = 0, P = 0, rpb = 0;
-    size_t sync_bytes = 0, part_bytes = 0;
-};
-
-// single-launch plan: P workgroups per image, rpb rows each (whole passes of the row-threads);
-// false when the switch is off or the grid could not be resident at once.  groups = 0: sizing
-// only (the largest group count the kernel takes, min(cin, 256), for the workspace bound)
-static bool gn_grid_plan(int n, int cin, int hw, int groups, GnGridPlan& pl) {
-    if (tuning().gn_grid <= 0 || n <= 0 || hw <= 0 || cin <= 0 || (cin & 7)) return false;
-    if (groups == 0) groups = cin < 256 ? cin : 256;
-    else if (groups < 0 || groups > 256 || cin % groups || cin / groups > 256) return false;
-    const int nch = cin >> 3;
-    if (nch > 512) return false;
-    const int cap = gn_grid_cap();
-    if (cap <= 0 || n > cap) return false;
-    pl.cpt = nch <= 256 ? 1 : 2;
-    const int R = pl.cpt == 1 ? 256 / nch : 1;
-    const int target = tuning().gn_grid_blocks < cap ? tuning().gn_grid_blocks : cap;
-    const int want = target / n > 0 ? target / n : 1;
-    int rpb = (hw + want - 1) / want;
-    rpb = (rpb + R - 1) / R * R;
-    pl.rpb = rpb;
-    pl.P = (hw + rpb - 1) / rpb;
-    if ((long)pl.P * n > cap) return false;
-    pl.sync_bytes = ((size_t)(kGnSyncHead + 2 * n) * sizeof(unsigned) + 15) / 16 * 16;
-    pl.part_bytes = (size_t)n * pl.P * groups * 2 * sizeof(float);
-    return true;
-}
-
-// ws: the barrier words (zeroed here, a memset node under capture) then the group pairs
-static int gn_grid_launch(const void* src0, const void* src1, int c0, int c1, int n, int hw, int pw, int groups,
-                          float eps, const float* gamma, const float* beta, int silu, void* out, void* ws,
-                          const GnGridPlan& pl, bool pad, hipStream_t s) {
-    const int cin = c0 + c1;
-    unsigned* sync = static_cast<unsigned*>(ws);
-    const int zm = tuning().gn_zero;
-    if (zm == 2) {
-        hipLaunchKernelGGL(gn_zero_kernel, dim3(1), dim3(64), 0, s, sync, (int)(pl.sync_bytes / 4));
-    } else if (zm == 1) {
-        if (hipMemsetD32Async((hipDeviceptr_t)ws, 0, pl.sync_bytes / 4, s) != hipSuccess) return check_launch();
-    } else if (hipMemsetAsync(ws, 0, pl.sync_bytes, s) != hipSuccess) {
-        return check_launch();
-    }
-    float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + pl.sync_bytes);
-    const size_t lds = (size_t)gn_grid_lds_floats(pl.cpt, cin, groups) * sizeof(float);
-    const dim3 grid(pl.P, n);
-#define C2D_GNG(C, PD)                                                                                          \
-    hipLaunchKernelGGL((gn_grid_kernel<C, PD>), grid, dim3(256), lds, s, (const f16*)src0, (const f16*)src1, c0, c1, \
-                       hw, pw, cin / groups, pl.rpb, eps, gamma, beta, silu, (f16*)out, sync, part)
-    if (pl.cpt == 1) {
-        if (pad) C2D_GNG(1, true); else C2D_GNG(1, false);
-    } else {
-        if (pad) C2D_GNG(2, true); else C2D_GNG(2, false);
-    }
-#undef C2D_GNG
-    return check_launch();
+    return gn_fused_cb(n, cin, groups) > 0 && hw <= gn_fused_max_hw();
 }
 
 
 extern "C" size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups) {
     if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return 0;
     if (gn_use_fused(n, c, hw, groups)) return 0;
-    const size_t multi = c2d_groupnorm_workspace_size(n, c, hw) + (size_t)n * c * 2 * sizeof(float);
-    GnGridPlan pl;
-    if (gn_grid_plan(n, c, hw, groups, pl) && pl.sync_bytes + pl.part_bytes > multi) return pl.sync_bytes + pl.part_bytes;
-    return multi;
+    return c2d_groupnorm_workspace_size(n, c, hw) + (size_t)n * c * 2 * sizeof(float);
 }
 
 extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups, float eps,
@@ -1075,9 +707,6 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
         return check_launch();
     }
     if (!ws || ws_bytes < c2d_groupnorm_run_workspace_size(n, cin, hw, groups) || !aligned16(ws)) return C2D_E_ARG;
-    GnGridPlan pl;
-    if (gn_grid_plan(n, cin, hw, groups, pl))
-        return gn_grid_launch(src0, src1, c0, c1, n, hw, 0, groups, eps, gamma, beta, silu, out, ws, pl, false, s);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
     float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
     float* shift = scale + (size_t)n * cin;
@@ -1088,11 +717,7 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
 
 extern "C" size_t c2d_groupnorm_pad_workspace_size(int n, int c, int h, int w) {
     if (n <= 0 || c <= 0 || h <= 0 || w <= 0) return 0;
-    const size_t multi = c2d_groupnorm_workspace_size(n, c, h * w) + (size_t)n * c * 2 * sizeof(float);
-    GnGridPlan pl;   // no group count here: sized for the most groups the kernel takes
-    if (gn_grid_plan(n, c, h * w, 0, pl) && pl.sync_bytes + pl.part_bytes > multi)
-        return pl.sync_bytes + pl.part_bytes;
-    return multi;
+    return c2d_groupnorm_workspace_size(n, c, h * w) + (size_t)n * c * 2 * sizeof(float);
 }
 
 extern "C" int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int c1, int n, int h, int w, int groups,
@@ -1106,10 +731,6 @@ extern "C" int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int
     if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out) || !aligned16(ws)) return C2D_E_ALIGN;
     const int hw = h * w;
     if (ws_bytes < c2d_groupnorm_pad_workspace_size(n, cin, h, w)) return C2D_E_ARG;
-    GnGridPlan pl;
-    if (gn_grid_plan(n, cin, hw, groups, pl))
-        return gn_grid_launch(src0, src1, c0, c1, n, hw, w + 2, groups, eps, gamma, beta, silu, out, ws, pl, true,
-                              (hipStream_t)stream);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
     float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
     float* shift = scale + (size_t)n * cin;

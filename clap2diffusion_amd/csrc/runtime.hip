@@ -38,14 +38,6 @@ const Tuning& tuning() {
         t.gn_apply_blocks = env_int("C2D_GN_APPLY_BLOCKS", 2048);
         if (t.gn_apply_blocks < 64) t.gn_apply_blocks = 2048;
         t.gn_fused_hw = env_int("C2D_GN_FUSED_HW", 256);
-        // single-launch GroupNorm: 0 off (multi-launch / per-chunk kernels), 1 for the images the
-        // three-launch path ran, 2 for every image
-        t.gn_grid = env_int("C2D_GN_GRID", 1);
-        t.gn_grid_blocks = env_int("C2D_GN_GRID_BLOCKS", 512);   // workgroups per launch (target)
-        if (t.gn_grid_blocks < 8) t.gn_grid_blocks = 512;
-        // barrier-word zeroing per call: 2 a one-wave kernel; 0 / 1 hipMemsetAsync / hipMemsetD32Async
-        // (A/B only: under graph replay the captured memset node left garbage from the second replay on)
-        t.gn_zero = env_int("C2D_GN_ZERO", 2);
 #ifdef C2D_ENABLE_ABLATION
         t.gemm_abl = env_int("C2D_GEMM_ABL", 0);
         t.attn_abl = env_int("C2D_ATTN_ABL", 0);

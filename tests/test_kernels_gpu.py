@@ -789,114 +789,6 @@ def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
     assert torch.equal(out, again)
 
 
-def _gn_call(x0, x1, groups, eps, gamma, beta, silu, pad=False, ws_extra=0):
-    """c2d_groupnorm / c2d_groupnorm_pad through ctypes with a caller-visible workspace
-    (the single-launch kernel's barrier words live at its start: word 0 counts poll timeouts)."""
-    from clap2diffusion_amd import _lib
-    import ctypes
-    lib = _lib.lib()
-    n, h, w, c0 = x0.shape
-    c1 = x1.shape[-1] if x1 is not None else 0
-    c = c0 + c1
-    p = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)
-    if pad:
-        wsb = lib.c2d_groupnorm_pad_workspace_size(n, c, h, w)
-        out = torch.empty(n, h + 2, w + 2, c, dtype=torch.float16, device=x0.device)
-    else:
-        wsb = lib.c2d_groupnorm_run_workspace_size(n, c, h * w, groups)
-        out = torch.empty(n, h, w, c, dtype=torch.float16, device=x0.device)
-    ws = torch.full(((wsb + ws_extra + 15) // 16 * 4,), 7, dtype=torch.int32, device=x0.device)   # poisoned
-    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    if pad:
-        rc = lib.c2d_groupnorm_pad(p(x0), p(x1), c0, c1, n, h, w, groups, eps, p(gamma), p(beta), int(silu),
-                                   p(out), p(ws), wsb, s)
-    else:
-        rc = lib.c2d_groupnorm(p(x0), p(x1), c0, c1, n, h * w, groups, eps, p(gamma), p(beta), int(silu), p(out),
-                               p(ws), wsb, s)
-    assert rc == 0, rc
-    torch.cuda.synchronize()
-    return out, ws
-
-
-# c2d_groupnorm for hw > 256 runs ONE kernel (statistics -> per-image in-launch barrier -> fold ->
-# apply; norm.hip gn_grid_kernel).  Against the explicit three-launch path (c2d_groupnorm_stats +
-# c2d_groupnorm_apply: same per-thread moments, a different fixed fold order) it agrees to within
-# the fp16 rounding of the output; against torch fp32 it meets the one-call bar.  The barrier words
-# at the workspace start (poisoned before the call) come back with no poll timeouts and every image's
-# arrival count back at zero.
-@pytest.mark.parametrize("n,h,w,c0,c1,groups,silu", [
-    (2, 64, 64, 320, 0, 32, True),        # c2 level 0: 228 workgroups per image
-    (16, 64, 64, 320, 0, 32, True),       # c3 level 0: 32 per image
-    (2, 32, 32, 640, 320, 32, False),     # concat seam inside a group
-    (1, 128, 128, 256, 0, 32, True),      # VAE up-block width
-    (3, 17, 23, 2560, 1280, 32, True),    # ragged image, 480 chunks per pixel (two chunks per thread)
-    (5, 20, 20, 320, 0, 64, False),       # 64 groups, cpg 5
-])
-def test_groupnorm_single_launch(dev, n, h, w, c0, c1, groups, silu):
-    c = c0 + c1
-    x0 = (gen(n, c0, h, w, seed=70) * 1.5 + 0.7)
-    x1 = gen(n, c1, h, w, seed=71) * 3 - 1 if c1 else None
-    gamma, beta = gen(c, seed=72) * 0.1 + 1, gen(c, seed=73) * 0.1
-    a = nhwc(x0).half().to(dev)
-    b = nhwc(x1).half().to(dev) if c1 else None
-    gd, bd = gamma.float().to(dev), beta.float().to(dev)
-    out, ws = _gn_call(a, b, groups, 1e-5, gd, bd, silu)
-    assert ws[0].item() == 0, "barrier poll timed out"
-    assert (ws[4:4 + 2 * n:2] == 0).all(), "arrival counts must return to zero"
-    ref = F.group_norm(torch.cat([nchw(a.float().cpu())] + ([nchw(b.float().cpu())] if c1 else []), 1),
-                       groups, gamma, beta, 1e-5)
-    if silu:
-        ref = F.silu(ref)
-    close(nchw(out), ref, tol_max=5e-3, tol_l2=1e-3)
-    gn = ops.group_norm_stats(a, groups, 1e-5, gd, bd, x2=b)
-    multi = ops.group_norm_apply(a, gn, silu, x2=b)
-    diff = (out.float() - multi.float()).abs()
-    assert diff.max().item() <= 2e-3 * max(1.0, multi.float().abs().max().item()), diff.max().item()
-    again, _ = _gn_call(a, b, groups, 1e-5, gd, bd, silu)
-    assert torch.equal(out, again), "single-launch GroupNorm must be run-to-run bit-identical"
-    pad, wsp = _gn_call(a, b, groups, 1e-5, gd, bd, silu, pad=True)
-    assert wsp[0].item() == 0
-    assert torch.equal(pad[:, 1:-1, 1:-1], out), "padded form's interior == the plain form"
-    assert (pad[:, 0] == 0).all() and (pad[:, -1] == 0).all() and (pad[:, :, 0] == 0).all() and (pad[:, :, -1] == 0).all()
-
-
-def test_groupnorm_single_launch_many_images(dev):
-    """One workgroup per image up to the resident-grid cap (CUs x 2), the three-launch path beyond
-    it: both agree with torch; images far apart in the grid never share a barrier."""
-    for n in (400, 600):
-        x = (gen(n, 64, 17, 17, seed=74) + torch.arange(n).view(n, 1, 1, 1) * 0.01)
-        a = nhwc(x).half().to(dev)
-        g, b = torch.ones(64, device=dev), torch.zeros(64, device=dev)
-        out, ws = _gn_call(a, None, 32, 1e-5, g, b, False)
-        ref = F.group_norm(nchw(a.float().cpu()), 32, None, None, 1e-5)
-        close(nchw(out), ref, tol_max=5e-3, tol_l2=1e-3)
-
-
-def test_groupnorm_single_launch_graph_replay(dev):
-    """Captured (a memset node re-zeroes the barrier words each replay) and replayed back to back
-    with a different-shaped norm in between: every replay equals the eager result bit for bit."""
-    a = nhwc(gen(2, 320, 64, 64, seed=75) + 0.2).half().to(dev)
-    b = nhwc(gen(4, 640, 32, 32, seed=76)).half().to(dev)
-    g1, b1 = torch.ones(320, device=dev), torch.zeros(320, device=dev)
-    g2, b2 = torch.ones(640, device=dev) * 0.5, torch.ones(640, device=dev) * 0.1
-    eager1 = ops.group_norm(a, 32, 1e-5, g1, b1, True)
-    eager2 = ops.group_norm(b, 32, 1e-6, g2, b2, False, pad=True)
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        ops.group_norm(a, 32, 1e-5, g1, b1, True)
-    torch.cuda.current_stream().wait_stream(s)
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        o1 = ops.group_norm(a, 32, 1e-5, g1, b1, True)
-        o2 = ops.group_norm(b, 32, 1e-6, g2, b2, False, pad=True)
-        o3 = ops.group_norm(a, 32, 1e-5, g1, b1, True)
-    for _ in range(5):
-        graph.replay()
-        torch.cuda.synchronize()
-        assert torch.equal(o1, eager1) and torch.equal(o3, eager1) and torch.equal(o2, eager2)
-
-
 # VAE widths: the planner's 256x128 (128 channels) and 256x256 (256 / 512 channels)
 # variants of the 32x32 tile; torch fp32 on the device is the reference
 @pytest.mark.parametrize("n,h,cin,cout", [
