@@ -17,11 +17,13 @@ __device__ __forceinline__ float gn_read(const f16* s0, const f16* s1, int c0, i
     return (float)((c < c0) ? s0[pix * c0 + c] : s1[pix * c1 + (c - c0)]);
 }
 
-template <int CPT>
+// GP: write per-GROUP pairs ws[n][blk][groups][2] instead (the block's channel totals folded over
+// each group's channels in a fixed order, in LDS) -- the input of gn_apply_fold_kernel
+template <int CPT, bool GP = false>
 __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
                                                          int c0, int c1, int hw, int cpg, int rows_per_block,
                                                          float* __restrict__ ws) {
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [R][cin*2]
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [R][cin*2] (CPT 1), then GP: [cin*2]
     const int cin = c0 + c1, nch = cin >> 3;
     const int n = blockIdx.y;
     const int t = threadIdx.x;
@@ -101,6 +103,44 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const f16* __restrict__
             for (int q = 0; q < CPT; ++q)
                 if (q == 0 || ch_base + q * 256 < nch) acc8(ld8(pix, q), q);
         }
+    }
+    if constexpr (GP) {
+        // channel totals of the block (fixed row order) -> LDS -> per group, fixed channel order
+        float* chs = red + (CPT == 1 ? R * cin * 2 : 0);
+        if (CPT == 1) {
+            if (active) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    red[(r0 * cin + ch_base * 8 + i) * 2 + 0] = sum[0][i];
+                    red[(r0 * cin + ch_base * 8 + i) * 2 + 1] = sq[0][i];
+                }
+            }
+            __syncthreads();
+            for (int c = t; c < cin; c += 256) {
+                float a = 0.f, b = 0.f;
+                for (int r = 0; r < R; ++r) { a += red[(r * cin + c) * 2]; b += red[(r * cin + c) * 2 + 1]; }
+                chs[c * 2] = a;
+                chs[c * 2 + 1] = b;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                const int ch = ch_base + q * 256;
+                if (ch >= nch) continue;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) { chs[(ch * 8 + i) * 2] = sum[q][i]; chs[(ch * 8 + i) * 2 + 1] = sq[q][i]; }
+            }
+        }
+        __syncthreads();
+        const int groups = cin / cpg;
+        float* dst = ws + ((size_t)n * gridDim.x + blockIdx.x) * groups * 2;
+        for (int g = t; g < groups; g += 256) {
+            float a = 0.f, b = 0.f;
+            for (int i = 0; i < cpg; ++i) { a += chs[(g * cpg + i) * 2]; b += chs[(g * cpg + i) * 2 + 1]; }
+            dst[g * 2] = a;
+            dst[g * 2 + 1] = b;
+        }
+        return;
     }
     // block reduction over the R row-threads sharing a channel chunk
     if (CPT == 1) {
@@ -236,6 +276,125 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s
         for (int i = 0; i < 8; ++i) {
             av[q][i] = scale[(size_t)n * cin + c + i];
             bv[q][i] = shift[(size_t)n * cin + c + i];
+        }
+    }
+    if constexpr (PAD) {
+        const int w = pw - 2, ph = hw / w + 2, npix = ph * pw;
+        const size_t pimg = (size_t)n * npix;
+#pragma unroll 2
+        for (int pp = blockIdx.x * R + r0; pp < npix; pp += gridDim.x * R) {
+            const int py = pp / pw, px = pp - py * pw;
+            const bool inner = py >= 1 && py < ph - 1 && px >= 1 && px < pw - 1;
+            const size_t gp = img + (inner ? (py - 1) * w + (px - 1) : 0);
+#pragma unroll
+            for (int q = 0; q < CPT; ++q) {
+                if (!on[q]) continue;
+                f16x8 o = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+                if (inner) {
+                    const f16x8 v = *reinterpret_cast<const f16x8*>(src[q] + gp * ld[q]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float y = fmaf((float)v[j], av[q][j], bv[q][j]);
+                        if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                        o[j] = (f16)y;
+                    }
+                }
+                *reinterpret_cast<f16x8*>(out + (pimg + pp) * cin + cc[q]) = o;
+            }
+        }
+        return;
+    }
+#pragma unroll 4
+    for (int pix = blockIdx.x * R + r0; pix < hw; pix += gridDim.x * R) {
+        const size_t gp = img + pix;
+#pragma unroll
+        for (int q = 0; q < CPT; ++q) {
+            if (!on[q]) continue;
+            const f16x8 v = *reinterpret_cast<const f16x8*>(src[q] + gp * ld[q]);
+            f16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float y = fmaf((float)v[j], av[q][j], bv[q][j]);
+                if (silu) y = y * __builtin_amdgcn_rcpf(1.0f + __expf(-y));
+                o[j] = (f16)y;
+            }
+            *reinterpret_cast<f16x8*>(out + gp * cin + cc[q]) = o;
+        }
+    }
+}
+
+// GroupNorm apply that folds the statistics itself (no finalize launch): every workgroup of
+// image n first folds the nblk per-group pairs gn_partial_kernel<., true> wrote (a few KB,
+// L2-resident; 256 / groups threads per group, fixed order, fp64), forms mean / rstd and
+// gn_finalize_kernel's per-channel affine for its own channels, then walks its pixels as
+// gn_apply_kernel does (PAD: the zero-bordered layout).  Same statistics in every workgroup of
+// an image: the fold order does not depend on the workgroup.
+template <int CPT, bool PAD>
+__global__ void __launch_bounds__(256) gn_apply_fold_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
+                                                            int c0, int c1, int hw, int cpg, int nblk, float eps,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ ws, int silu,
+                                                            f16* __restrict__ out, int pw = 0) {
+    __shared__ double dacc[512];   // [256][2] fold partials
+    __shared__ float gmr[512];     // [groups][2] mean, rstd (groups <= 256)
+    const int cin = c0 + c1, nch = cin >> 3, groups = cin / cpg;
+    const int L = nch < 256 ? nch : 256, R = 256 / L;
+    const int t = threadIdx.x, lane_c = t % L, r0 = t / L;
+    const int n = blockIdx.y;
+    const size_t img = (size_t)n * hw;
+    const int parts = 256 / groups;
+    if (t < parts * groups) {
+        const int g = t % groups, pt = t / groups;
+        const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * groups + g;
+        double a = 0.0, b = 0.0;
+        int k = pt;
+        for (; k + 3 * parts < nblk; k += 4 * parts) {
+            const float2 v0 = wp[(size_t)k * groups], v1 = wp[(size_t)(k + parts) * groups];
+            const float2 v2 = wp[(size_t)(k + 2 * parts) * groups], v3 = wp[(size_t)(k + 3 * parts) * groups];
+            a += (double)v0.x; b += (double)v0.y;
+            a += (double)v1.x; b += (double)v1.y;
+            a += (double)v2.x; b += (double)v2.y;
+            a += (double)v3.x; b += (double)v3.y;
+        }
+        for (; k < nblk; k += parts) {
+            const float2 v = wp[(size_t)k * groups];
+            a += (double)v.x; b += (double)v.y;
+        }
+        dacc[t * 2] = a;
+        dacc[t * 2 + 1] = b;
+    }
+    __syncthreads();
+    if (t < groups) {
+        double a = 0.0, b = 0.0;
+        for (int pt = 0; pt < parts; ++pt) { a += dacc[(pt * groups + t) * 2]; b += dacc[(pt * groups + t) * 2 + 1]; }
+        const double cnt = (double)hw * cpg;
+        const double m1 = a / cnt;
+        double var = b / cnt - m1 * m1;
+        if (var < 0.0) var = 0.0;
+        gmr[t * 2] = (float)(gn_read(s0, s1, c0, c1, img, t * cpg) + m1);
+        gmr[t * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    }
+    __syncthreads();
+    if (r0 >= R) return;
+    float av[CPT][8], bv[CPT][8];
+    const f16* src[CPT];
+    int ld[CPT], cc[CPT];
+    bool on[CPT];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+        const int ch = lane_c + q * 256;
+        on[q] = ch < nch;
+        cc[q] = (on[q] ? ch : 0) * 8;
+        const int c = cc[q];
+        src[q] = (c < c0) ? (s0 + c) : (s1 + (c - c0));
+        ld[q] = (c < c0) ? c0 : c1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int gl = (c + i) / cpg;
+            const float sc = gamma[c + i] * gmr[gl * 2 + 1];
+            av[q][i] = sc;
+            bv[q][i] = beta[c + i] - gmr[gl * 2] * sc;
         }
     }
     if constexpr (PAD) {
@@ -684,6 +843,43 @@ static bool gn_use_fused(int n, int cin, int hw, int groups) {
 }
 
 
+// partial (per-group pairs) + apply-with-fold: two launches where c2d_groupnorm_stats +
+// c2d_groupnorm_apply take three (C2D_GN_FOLD=0 restores those, A/B only).  Needs groups <= 256.
+static bool gn_use_fold(int cin, int groups) { return tuning().gn_fold != 0 && groups <= 256 && (cin >> 3) <= 512; }
+
+static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n, int hw, int pw, int groups,
+                       float eps, const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s) {
+    const int cin = c0 + c1, nch = cin >> 3, cpg = cin / groups;
+    const int rows_per_block = gn_rows_per_block(n, cin, hw);
+    const int nblk = gn_blocks(n, cin, hw);
+    const dim3 pgrid(nblk, n);
+    if (nch <= 256) {
+        const size_t lds = ((size_t)(256 / nch) * cin * 2 + (size_t)cin * 2) * sizeof(float);
+        hipLaunchKernelGGL((gn_partial_kernel<1, true>), pgrid, dim3(256), lds, s, (const f16*)src0, (const f16*)src1,
+                           c0, c1, hw, cpg, rows_per_block, (float*)ws);
+    } else {
+        hipLaunchKernelGGL((gn_partial_kernel<2, true>), pgrid, dim3(256), (size_t)cin * 2 * sizeof(float), s,
+                           (const f16*)src0, (const f16*)src1, c0, c1, hw, cpg, rows_per_block, (float*)ws);
+    }
+    const int L = nch < 256 ? nch : 256, R = 256 / L;
+    const int npix = pw ? (hw / (pw - 2) + 2) * pw : hw;
+    int bx = (gn_apply_blocks() + n - 1) / n;
+    const int maxb = (npix + R - 1) / R;
+    if (bx > maxb) bx = maxb;
+    if (bx < 1) bx = 1;
+    const dim3 agrid(bx, n);
+#define C2D_GNF(C, PD)                                                                                           \
+    hipLaunchKernelGGL((gn_apply_fold_kernel<C, PD>), agrid, dim3(256), 0, s, (const f16*)src0, (const f16*)src1, c0, \
+                       c1, hw, cpg, nblk, eps, gamma, beta, (const float*)ws, silu, (f16*)out, pw)
+    if (nch <= 256) {
+        if (pw) C2D_GNF(1, true); else C2D_GNF(1, false);
+    } else {
+        if (pw) C2D_GNF(2, true); else C2D_GNF(2, false);
+    }
+#undef C2D_GNF
+    return check_launch();
+}
+
 extern "C" size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups) {
     if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return 0;
     if (gn_use_fused(n, c, hw, groups)) return 0;
@@ -707,6 +903,8 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
         return check_launch();
     }
     if (!ws || ws_bytes < c2d_groupnorm_run_workspace_size(n, cin, hw, groups) || !aligned16(ws)) return C2D_E_ARG;
+    if (gn_use_fold(cin, groups))   // group pairs fit the per-channel partial region (groups <= cin)
+        return gn_fold_run(src0, src1, c0, c1, n, hw, 0, groups, eps, gamma, beta, silu, out, ws, s);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
     float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
     float* shift = scale + (size_t)n * cin;
@@ -731,6 +929,9 @@ extern "C" int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int
     if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out) || !aligned16(ws)) return C2D_E_ALIGN;
     const int hw = h * w;
     if (ws_bytes < c2d_groupnorm_pad_workspace_size(n, cin, h, w)) return C2D_E_ARG;
+    if (gn_use_fold(cin, groups))
+        return gn_fold_run(src0, src1, c0, c1, n, hw, w + 2, groups, eps, gamma, beta, silu, out, ws,
+                           (hipStream_t)stream);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
     float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
     float* shift = scale + (size_t)n * cin;

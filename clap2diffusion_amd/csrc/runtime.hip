@@ -38,6 +38,7 @@ const Tuning& tuning() {
         t.gn_apply_blocks = env_int("C2D_GN_APPLY_BLOCKS", 2048);
         if (t.gn_apply_blocks < 64) t.gn_apply_blocks = 2048;
         t.gn_fused_hw = env_int("C2D_GN_FUSED_HW", 256);
+        t.gn_fold = env_int("C2D_GN_FOLD", 1);   // 0: partial + finalize + apply (A/B)
 #ifdef C2D_ENABLE_ABLATION
         t.gemm_abl = env_int("C2D_GEMM_ABL", 0);
         t.attn_abl = env_int("C2D_ATTN_ABL", 0);

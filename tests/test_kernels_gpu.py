@@ -789,6 +789,35 @@ def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
     assert torch.equal(out, again)
 
 
+# c2d_groupnorm / c2d_groupnorm_pad above 256 pixels: per-group partial pairs, then an apply
+# kernel that folds them itself (two launches).  Against the three-launch API (c2d_groupnorm_stats
+# -> per-channel partials + finalize, then c2d_groupnorm_apply: same per-thread moments, another
+# fixed fold order) the outputs agree to the fp16 rounding of the result.
+@pytest.mark.parametrize("n,h,w,c0,c1,groups,silu", [
+    (2, 64, 64, 320, 0, 32, True),        # c2 level 0
+    (16, 64, 64, 320, 0, 32, True),       # c3 level 0
+    (2, 32, 32, 640, 320, 32, False),     # concat seam inside a group
+    (3, 17, 23, 2560, 1280, 32, True),    # ragged image, two channel chunks per thread
+    (5, 20, 20, 320, 0, 64, False),       # 64 groups, cpg 5
+])
+def test_groupnorm_two_launch_matches_three(dev, n, h, w, c0, c1, groups, silu):
+    c = c0 + c1
+    x0 = gen(n, c0, h, w, seed=70) * 1.5 + 0.7
+    x1 = gen(n, c1, h, w, seed=71) * 3 - 1 if c1 else None
+    gamma, beta = (gen(c, seed=72) * 0.1 + 1).to(dev), (gen(c, seed=73) * 0.1).to(dev)
+    a = nhwc(x0).half().to(dev)
+    b = nhwc(x1).half().to(dev) if c1 else None
+    out = ops.group_norm(a, groups, 1e-5, gamma, beta, silu, x2=b)
+    multi = ops.group_norm_apply(a, ops.group_norm_stats(a, groups, 1e-5, gamma, beta, x2=b), silu, x2=b)
+    diff = (out.float() - multi.float()).abs().max().item()
+    assert diff <= 2e-3 * max(1.0, multi.float().abs().max().item()), diff
+    pad = ops.group_norm(a, groups, 1e-5, gamma, beta, silu, x2=b, pad=True)
+    assert torch.equal(pad[:, 1:-1, 1:-1], out), "padded form's interior == the plain form"
+    border = torch.ones(h + 2, w + 2, dtype=torch.bool, device=dev)
+    border[1:-1, 1:-1] = False
+    assert (pad[:, border] == 0).all()
+
+
 # VAE widths: the planner's 256x128 (128 channels) and 256x256 (256 / 512 channels)
 # variants of the 32x32 tile; torch fp32 on the device is the reference
 @pytest.mark.parametrize("n,h,cin,cout", [
