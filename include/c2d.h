@@ -171,10 +171,12 @@ int c2d_groupnorm_apply(const void* src0, const void* src1, int c0, int c1, int 
  * norms) needs.  Small images (hw <= 256 pixels) run a single kernel: one
  * workgroup per (image, chunk of whole groups) computes the statistics, folds them in
  * a fixed order and applies in a second pass over the L2 / MALL-resident slab.
- * Larger ones run c2d_groupnorm_stats + c2d_groupnorm_apply with their partials and
- * tables carved from ws (>= c2d_groupnorm_run_workspace_size(n, c0+c1, hw, groups)
- * bytes, 16-B aligned; the size is 0 -- ws may be NULL -- when the single kernel
- * runs).  Deterministic either way.
+ * Larger ones run two kernels: per-block partial moments folded per group (ws >=
+ * c2d_groupnorm_run_workspace_size(n, c0+c1, hw, groups) bytes, 16-B aligned; the size is
+ * 0 -- ws may be NULL -- when the single kernel runs), then an apply kernel whose
+ * workgroups fold an image's group partials in a fixed order themselves (no separate
+ * finalize launch; up to 256 groups, else c2d_groupnorm_stats + c2d_groupnorm_apply).
+ * Deterministic either way.
  */
 size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups);
 int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups,
