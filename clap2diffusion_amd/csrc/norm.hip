@@ -728,19 +728,19 @@ static int gn_apply_blocks() { return tuning().gn_apply_blocks; }
 // rows per partial block: about gn_target_blocks() blocks over the launch, but at most
 // ~32 per image -- the finalize folds an image's partials serially (fixed order), so at
 // small N (c2: N = 2, 64^2) 228 blocks per image made it a 9.2-us latency chain per call
-static int gn_rows_per_block(int n, int c, int hw) {
+static int gn_rows_per_block(int n, int c, int hw, int cap = 32) {
     const int nch = c >> 3;
     const int r = nch <= 256 ? 256 / nch : 1;
     const long tb = gn_target_blocks();
     long want = ((long)n * hw + tb - 1) / tb;
-    if (want < (hw + 31) / 32) want = (hw + 31) / 32;
+    if (want < (hw + cap - 1) / cap) want = (hw + cap - 1) / cap;
     if (want < r) want = r;
     if (want > 128) want = 128;
     return (int)((want + r - 1) / r * r);
 }
 
-static int gn_blocks(int n, int c, int hw) {
-    const int rpb = gn_rows_per_block(n, c, hw);
+static int gn_blocks(int n, int c, int hw, int cap = 32) {
+    const int rpb = gn_rows_per_block(n, c, hw, cap);
     return (hw + rpb - 1) / rpb;
 }
 
@@ -850,8 +850,9 @@ static bool gn_use_fold(int cin, int groups) { return tuning().gn_fold != 0 && g
 static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n, int hw, int pw, int groups,
                        float eps, const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s) {
     const int cin = c0 + c1, nch = cin >> 3, cpg = cin / groups;
-    const int rows_per_block = gn_rows_per_block(n, cin, hw);
-    const int nblk = gn_blocks(n, cin, hw);
+    const int cap = tuning().gn_fold_cap;   // partial blocks per image (the apply's fold is parallel)
+    const int rows_per_block = gn_rows_per_block(n, cin, hw, cap);
+    const int nblk = gn_blocks(n, cin, hw, cap);
     const dim3 pgrid(nblk, n);
     if (nch <= 256) {
         const size_t lds = ((size_t)(256 / nch) * cin * 2 + (size_t)cin * 2) * sizeof(float);
@@ -880,10 +881,17 @@ static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n
     return check_launch();
 }
 
+// the fold path's group pairs: n x partial blocks x groups x {sum, sumsq}
+static size_t gn_fold_ws_bytes(int n, int c, int hw, int groups) {
+    return (size_t)n * gn_blocks(n, c, hw, tuning().gn_fold_cap) * groups * 2 * sizeof(float);
+}
+
 extern "C" size_t c2d_groupnorm_run_workspace_size(int n, int c, int hw, int groups) {
     if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return 0;
     if (gn_use_fused(n, c, hw, groups)) return 0;
-    return c2d_groupnorm_workspace_size(n, c, hw) + (size_t)n * c * 2 * sizeof(float);
+    const size_t multi = c2d_groupnorm_workspace_size(n, c, hw) + (size_t)n * c * 2 * sizeof(float);
+    const size_t fold = gn_fold_ws_bytes(n, c, hw, groups);
+    return fold > multi ? fold : multi;
 }
 
 extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1, int n, int hw, int groups, float eps,
@@ -903,7 +911,7 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
         return check_launch();
     }
     if (!ws || ws_bytes < c2d_groupnorm_run_workspace_size(n, cin, hw, groups) || !aligned16(ws)) return C2D_E_ARG;
-    if (gn_use_fold(cin, groups))   // group pairs fit the per-channel partial region (groups <= cin)
+    if (gn_use_fold(cin, groups))   // ws sized for the group pairs too (gn_fold_ws_bytes)
         return gn_fold_run(src0, src1, c0, c1, n, hw, 0, groups, eps, gamma, beta, silu, out, ws, s);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
     float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
@@ -915,7 +923,9 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
 
 extern "C" size_t c2d_groupnorm_pad_workspace_size(int n, int c, int h, int w) {
     if (n <= 0 || c <= 0 || h <= 0 || w <= 0) return 0;
-    return c2d_groupnorm_workspace_size(n, c, h * w) + (size_t)n * c * 2 * sizeof(float);
+    const size_t multi = c2d_groupnorm_workspace_size(n, c, h * w) + (size_t)n * c * 2 * sizeof(float);
+    const size_t fold = gn_fold_ws_bytes(n, c, h * w, c < 256 ? c : 256);   // the most groups the fold takes
+    return fold > multi ? fold : multi;
 }
 
 extern "C" int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int c1, int n, int h, int w, int groups,
