@@ -1,5 +1,7 @@
-"""Diagnostic: the single-launch GroupNorm's barrier words after eager calls and after graph
-replays (workspace allocated outside the capture, so it can be read back)."""
+"""Diagnostic for the removed single-launch GroupNorm (norm.hip at commit 818994c, C2D_GN_ZERO selected how
+its barrier words were zeroed): the words after eager calls and after graph replays (workspace allocated
+outside the capture, so it can be read back).  Against the current library c2d_groupnorm runs the
+two-launch path, which has no barrier words: the script then only checks replay == eager."""
 import ctypes
 import sys
 from pathlib import Path
