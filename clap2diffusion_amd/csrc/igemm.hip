@@ -1098,11 +1098,57 @@ static bool rr_eligible(const c2d_conv_desc* d) {
            d->oh == d->h && d->ow == d->w && d->kpad == 9 * d->c0;
 }
 
+// Image split of a quantisation tail.  A one-slice plan whose grid is whole rounds of the chip plus
+// at most a quarter round (c5's level-0 3x3 convs: 288 tiles of 256 x 320 on 256 CUs = one round
+// + 32 tiles, the second round 1/8 full) runs as two launches: the first n1 images, whose tiles fit
+// the whole rounds, on the plan; the rest on their own plan (split K over the idle CUs).  Only for
+// deep K (>= 16 steps, so the extra launch is small against a round) and the planner's own choice
+// (no override); returns n1, 0 = no split.
+static int tail_images(const c2d_conv_desc* d, const DmaPlan& pl) {
+    if (pl.split != 1 || d->n < 2 || d->pro != C2D_PRO_NONE || d->kpad / 64 < 16) return 0;
+    if (plan_override_tile() || plan_override_split() || !tuning().tail_split) return 0;
+    const DmaTile* t = nullptr;
+    for (const DmaTile& x : kDmaTiles)
+        if (x.id == pl.id) t = &x;
+    if (!t) return 0;   // the persistent tile (50) walks its own grid
+    const long hw = (long)d->oh * d->ow, slots = 256L * t->occ;
+    const long gx = (d->cout + t->bn - 1) / t->bn;
+    const long tiles = (d->n * hw + t->bm - 1) / t->bm * gx;
+    const long full = tiles / slots * slots, rem = tiles - full;
+    if (full == 0 || rem == 0 || rem > slots / 4) return 0;
+    int n1 = d->n - 1;
+    while (n1 > 0 && (n1 * hw + t->bm - 1) / t->bm * gx > full) --n1;
+    return n1;
+}
+
+// the descriptor of images [n1, n): every per-image pointer advanced by n1 images
+static c2d_conv_desc tail_desc(const c2d_conv_desc* d, int n1) {
+    c2d_conv_desc t = *d;
+    const size_t in_pix = (size_t)n1 * (d->src_pad ? (size_t)(d->h + 2) * (d->w + 2) : (size_t)d->h * d->w);
+    const size_t out_rows = (size_t)n1 * d->oh * d->ow;
+    t.n = d->n - n1;
+    t.src0 = static_cast<const f16*>(d->src0) + in_pix * d->c0;
+    if (d->src1) t.src1 = static_cast<const f16*>(d->src1) + in_pix * d->c1;
+    if (d->temb) t.temb = static_cast<const f16*>(d->temb) + (size_t)n1 * d->temb_ld;
+    if (d->resid) t.resid = static_cast<const f16*>(d->resid) + out_rows * d->resid_ld;
+    t.out = static_cast<f16*>(d->out) + out_rows * d->out_ld;
+    return t;
+}
+
+// split-K workspace of the tail launch (the head runs one slice)
+static size_t tail_ws_bytes(const c2d_conv_desc* d, int n1) {
+    const c2d_conv_desc t = tail_desc(d, n1);
+    const long Mt = (long)t.n * t.oh * t.ow;
+    const DmaPlan tp = plan_for(Mt, t.cout, t.kpad, t.act, pps_eligible(&t), t.ksize, rr_eligible(&t));
+    return tp.split > 1 ? (size_t)tp.split * Mt * t.cout * sizeof(float) : 0;
+}
+
 extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
     if (!dma_eligible(d)) return 0;
     const long M = (long)d->n * d->oh * d->ow;
     const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+    if (const int n1 = tail_images(d, pl)) return tail_ws_bytes(d, n1);
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
 
@@ -1125,7 +1171,28 @@ extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* 
     return C2D_OK;
 }
 
+static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed);
+
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
+    if (!d || !d->src0 || !d->weight || !d->out) return C2D_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (d->n >= 2 && d->ksize >= 1 && d->oh > 0 && d->ow > 0 && d->cout > 0 && d->kpad >= 64 && dma_eligible(d)) {
+        const long M = (long)d->n * d->oh * d->ow;
+        const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+        if (const int n1 = tail_images(d, pl)) {   // quantisation tail: whole rounds, then the rest
+            c2d_conv_desc head = *d;
+            head.n = n1;
+            const int rc = conv_run(&head, s, &pl);
+            if (rc != C2D_OK) return rc;
+            const c2d_conv_desc tail = tail_desc(d, n1);
+            return conv_run(&tail, s, nullptr);
+        }
+    }
+    return conv_run(d, s, nullptr);
+}
+
+// fixed: run this plan (the head of a tail split) instead of planning for d's own M
+static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed) {
     if (!d || !d->src0 || !d->weight || !d->out) return C2D_E_ARG;
     if (d->ksize != 1 && d->ksize != 3) return C2D_E_SHAPE;
     if (d->c1 > 0 && !d->src1) return C2D_E_ARG;
@@ -1175,7 +1242,6 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.M = d->n * d->oh * d->ow;
     if (p.M <= 0) return C2D_OK;
 
-    hipStream_t s = (hipStream_t)stream;
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
     const bool dma = dma_eligible(d);
     p.ksplit = 1;
@@ -1187,7 +1253,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        DmaPlan pl = plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+        DmaPlan pl = fixed ? *fixed : plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
         if (pl.split > 1) {
             const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
             if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {

@@ -789,6 +789,45 @@ def test_groupnorm_one_call(dev, n, h, c0, c1, groups, silu, eps):
     assert torch.equal(out, again)
 
 
+# Quantisation tail (igemm.hip tail_images): c5's level-0 convs plan one K slice on 288 tiles of
+# 256 x 320, so the first 7 images run that plan and the 8th its own -- every per-image pointer of
+# the tail launch (both sources, the time embedding, the residual, the output; the zero-bordered
+# source) is offset by 7 images.  Same numerics bar as every conv.
+@pytest.mark.parametrize("c0,c1,res,tmb,padded", [
+    (320, 0, True, False, False),     # ResnetBlock2D conv2 + residual
+    (320, 320, False, True, False),   # up-block conv1 over the skip concat + time embedding
+    (640, 320, True, True, False),    # 960 -> 320 with both epilogue terms
+    (320, 0, True, True, True),       # zero-bordered source
+])
+def test_conv_quantisation_tail(dev, c0, c1, res, tmb, padded):
+    n, h, cout = 8, 96, 320
+    cin = c0 + c1
+    assert ops.rowring_conv(n, h, h, cin, cout) is False
+    x = gen(n, cin, h, h, seed=171)
+    w = gen(cout, cin, 3, 3, seed=172, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=173)
+    r = gen(n, cout, h, h, seed=174) if res else None
+    te = gen(n, cout, seed=175) if tmb else None
+    ref = F.conv2d(x.half().float(), w, b, padding=1)
+    if te is not None:
+        ref = ref + te.half().float()[:, :, None, None]
+    if r is not None:
+        ref = ref + r.half().float()
+    wp, kp = ops.pack_conv_weight(w)
+    xd = nhwc(x).half().to(dev)
+    kw = dict(bias=b.float().to(dev), resid=nhwc(r).half().to(dev) if res else None,
+              temb=te.half().to(dev) if tmb else None)
+    with ops.record_conv_plans() as plans:
+        if padded:
+            xp = F.pad(xd.permute(0, 3, 1, 2), (1, 1, 1, 1)).permute(0, 2, 3, 1).contiguous()
+            out = ops.conv(xp, wp.to(dev), kp, cout, ksize=3, padded=True, **kw)
+        else:
+            x0, x1 = (xd[..., :c0].contiguous(), xd[..., c0:].contiguous()) if c1 else (xd, None)
+            out = ops.conv(x0, wp.to(dev), kp, cout, ksize=3, x2=x1, **kw)
+    assert plans == [(40, 1)], plans
+    close(nchw(out), ref)
+
+
 # c2d_groupnorm / c2d_groupnorm_pad above 256 pixels: per-group partial pairs, then an apply
 # kernel that folds them itself (two launches).  Against the three-launch API (c2d_groupnorm_stats
 # -> per-channel partials + finalize, then c2d_groupnorm_apply: same per-thread moments, another

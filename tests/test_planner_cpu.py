@@ -48,3 +48,24 @@ def test_table_split_needs_workspace_and_other_shapes_use_the_rules():
     assert _plan(320, 320, 2, 64, 3, ws=False) == (7, 1)
     # c3's level-0 resnet conv is not in the table: the rules' 256 x 320 ping-pong tile
     assert _plan(320, 320, 16, 64, 3) == (40, 1)
+
+
+
+def _ws(cin, cout, n, h, k):
+    import torch  # noqa: F401
+    from clap2diffusion_amd import _lib, ops
+    d = _lib.ConvDesc()
+    d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, n, h, h, h, h, k, 1
+    d.cout, d.kpad = cout, ops.kpad_of(k * k * cin)
+    return _lib.lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
+
+
+def test_quantisation_tail_reports_the_head_plan():
+    """c5's level-0 3x3 convs plan one K slice on 288 tiles of 256 x 320 (one round of 256 CUs +
+    32 tiles): c2d_conv2d_igemm runs the first 7 images on that plan and the 8th on its own plan
+    (igemm.hip tail_images; the tail's plan here fills the chip without split-K, so the call asks
+    for no workspace).  c2d_conv2d_igemm_plan reports the head's plan."""
+    assert _plan(320, 320, 8, 96, 3) == (40, 1)
+    assert _ws(320, 320, 8, 96, 3) == 0
+    assert _plan(320, 320, 1, 96, 3) == (3, 1)           # what the tail image runs
+    assert _plan(320, 320, 16, 64, 3) == (40, 1) and _ws(320, 320, 16, 64, 3) == 0   # c3: exact fit
