@@ -113,6 +113,56 @@ def _read_wav(path: str, max_seconds: float | None = None) -> tuple[np.ndarray, 
     return x.reshape(-1, ch).mean(axis=1), sr
 
 
+def _pcm_to_float(raw: bytes, width: int, big: bool) -> np.ndarray:
+    """Signed linear PCM of `width` bytes per sample -> float32 in [-1, 1)."""
+    if width == 1:
+        return np.frombuffer(raw, dtype=np.int8).astype(np.float32) / 128.0
+    if width == 3:
+        b = np.frombuffer(raw, dtype=np.uint8).reshape(-1, 3).astype(np.int32)
+        v = (b[:, 0] << 16 | b[:, 1] << 8 | b[:, 2]) if big else (b[:, 0] | b[:, 1] << 8 | b[:, 2] << 16)
+        return (np.where(v >= 1 << 23, v - (1 << 24), v)).astype(np.float32) / float(1 << 23)
+    dt = {2: "i2", 4: "i4"}[width]
+    return np.frombuffer(raw, dtype=(">" if big else "<") + dt).astype(np.float32) / float(2 ** (8 * width - 1))
+
+
+def _read_stdlib(mod, path: str, max_seconds: float | None) -> tuple[np.ndarray, int]:
+    """AIFF / AIFC (aifc) and Sun AU (sunau) through the standard library's readers: linear PCM
+    8 / 16 / 24 / 32-bit (big-endian; AIFC 'sowt' comes back big-endian from aifc) and the
+    companded codecs those modules expand to native-endian 16-bit (u-law / a-law / G.722)."""
+    with mod.open(path, "rb") as f:
+        ch, width, sr, n = f.getnchannels(), f.getsampwidth(), f.getframerate(), f.getnframes()
+        if max_seconds is not None:
+            n = min(n, int(max_seconds * sr))
+        raw = f.readframes(n)
+        comp = f.getcomptype()
+    comp = comp.decode() if isinstance(comp, bytes) else str(comp)
+    big = comp.upper() in ("NONE", "SOWT") or comp == "not compressed"
+    if width not in (1, 2, 3, 4):
+        raise ValueError(f"{path}: unsupported sample width {width}")
+    x = _pcm_to_float(raw[: len(raw) // (width * ch) * width * ch], width, big)
+    return x.reshape(-1, ch).mean(axis=1), sr
+
+
+def read_audio(path: str, max_seconds: float | None = None) -> tuple[np.ndarray, int]:
+    """(mono float32, native rate) of a WAV, AIFF / AIFC or Sun AU file, chosen by its header (the
+    containers this image decodes without librosa; reference scripts/inference.py:78 reads any
+    format librosa does).  max_seconds: keep the first max_seconds at the native rate."""
+    head = Path(path).read_bytes()[:12]
+    if head[:4] == b"RIFF" and head[8:12] == b"WAVE":
+        return _read_wav(path, max_seconds)
+    import warnings
+    with warnings.catch_warnings():   # aifc / sunau are deprecated from Python 3.11 on
+        warnings.simplefilter("ignore", DeprecationWarning)
+        if head[:4] == b"FORM" and head[8:12] in (b"AIFF", b"AIFC"):
+            import aifc
+            return _read_stdlib(aifc, path, max_seconds)
+        if head[:4] == b".snd":
+            import sunau
+            return _read_stdlib(sunau, path, max_seconds)
+    raise ValueError(f"{path}: not a RIFF/WAVE, AIFF/AIFC or Sun AU file (other formats need a decoder this "
+                     "image does not have: convert them first)")
+
+
 class AudioToImageInference:
     def __init__(self, checkpoint_dir="../checkpoints", device=None, seed: int = 0, height: int = 512,
                  width: int = 512, use_graph: bool = True, verbose: bool = True, sd_model_path=None,
@@ -202,7 +252,7 @@ class AudioToImageInference:
         if str(audio_path).startswith("synthetic:"):
             audio = synthetic_thunder(int(str(audio_path).split(":", 1)[1] or 0), duration)
         else:
-            x, sr = _read_wav(audio_path, max_seconds=duration)
+            x, sr = read_audio(audio_path, max_seconds=duration)
             if sr != SR:
                 from scipy.signal import resample_poly
                 g = np.gcd(sr, SR)

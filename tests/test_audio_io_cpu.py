@@ -1,4 +1,4 @@
-"""WAV decoding of AudioToImageInference.load_audio (reference scripts/inference.py:73-79:
+"""WAV / AIFF / AIFC / Sun AU decoding of AudioToImageInference.load_audio (reference scripts/inference.py:73-79:
 librosa.load(path, sr=48000, mono=True, duration=10), then peak normalisation).  librosa is
 absent here, so the resampler's numerics are not pinned to it (scipy polyphase vs soxr); what
 is checked: every RIFF/WAVE encoding the reader claims decodes to the samples written, channels
@@ -71,3 +71,79 @@ def test_non_wav_is_refused(tmp_path):
     p.write_bytes(b"ID3\x03\x00" + bytes(100))
     with pytest.raises(ValueError, match="RIFF/WAVE"):
         _read_wav(str(p))
+
+
+def _write_stdlib(mod, path, x, sr, width, comp=None):
+    """AIFF / AIFC / Sun AU through the standard library's writers; x float [frames, ch]."""
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", DeprecationWarning)
+        f = mod.open(str(path), "wb")
+        f.setnchannels(x.shape[1])
+        f.setframerate(sr)
+        if comp is not None:
+            f.setcomptype(*comp)
+            f.setsampwidth(2)
+            v = np.round(x * 32767).astype(np.int16)
+            f.writeframes(v.astype("<i2" if comp[0] in (b"ULAW", "ULAW", b"ALAW") else ">i2").tobytes())
+        else:
+            if mod.__name__ == "sunau":
+                f.setcomptype("NONE", "not compressed")   # sunau's writer defaults to u-law
+            f.setsampwidth(width)
+            scale = 2 ** (8 * width - 1)
+            v = np.clip(np.round(x.astype(np.float64) * scale), -scale, scale - 1).astype(np.int64).reshape(-1)
+            if width == 3:
+                v = np.where(v < 0, v + (1 << 24), v)
+                raw = np.stack([(v >> 16) & 255, (v >> 8) & 255, v & 255], 1).astype(np.uint8).tobytes()
+            else:
+                raw = v.astype({1: "i1", 2: ">i2", 4: ">i4"}[width]).tobytes()
+            f.writeframes(raw)
+        f.close()
+
+
+@pytest.mark.parametrize("kind,width,comp,tol", [
+    ("aiff", 1, None, 1 / 64), ("aiff", 2, None, 1e-4), ("aiff", 3, None, 1e-6), ("aiff", 4, None, 1e-6),
+    ("aifc", 2, (b"ULAW", b""), 0.03),
+    ("au", 1, None, 1 / 64), ("au", 2, None, 1e-4), ("au", 3, None, 1e-6), ("au", 4, None, 1e-6),
+    ("au", 2, ("ULAW", "CCITT G.711 u-law"), 0.03),
+])
+def test_aiff_and_au_decode(tmp_path, kind, width, comp, tol):
+    """reference scripts/inference.py:78 reads any container librosa does; this image has no
+    decoder beyond the standard library, so load_audio takes WAV (above), AIFF / AIFC and Sun AU:
+    every linear width and the u-law codec decode to the samples written, channels averaged."""
+    import aifc
+    import sunau
+    from clap2diffusion_amd.pipeline import read_audio
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-0.9, 0.9, size=(800, 2)).astype(np.float32)
+    p = tmp_path / f"a.{kind}"
+    if kind == "au" and width == 1:   # sunau writes 8-bit as u-law: linear 8-bit (encoding 2) by hand
+        body = np.clip(np.round(x.astype(np.float64) * 128), -128, 127).astype(np.int8).tobytes()
+        hdr = b".snd" + b"".join(v.to_bytes(4, "big") for v in (24, len(body), 2, 16000, 2))
+        p.write_bytes(hdr + body)
+    else:
+        _write_stdlib(sunau if kind == "au" else aifc, p, x, 16000, width, comp)
+    y, sr = read_audio(str(p))
+    assert sr == 16000 and y.dtype == np.float32 and y.shape == (800,)
+    assert np.abs(y - x.mean(axis=1)).max() <= tol + 1e-7
+    y2, _ = read_audio(str(p), max_seconds=0.01)
+    assert y2.shape == (160,) and np.array_equal(y2, y[:160])
+
+
+def test_load_audio_reads_aiff_and_refuses_unknown(tmp_path):
+    import aifc
+    from clap2diffusion_amd.pipeline import read_audio
+    sr = 44100
+    t = np.arange(int(11 * sr)) / sr
+    x = (0.5 * np.sin(2 * np.pi * 1000.0 * t))[:, None].astype(np.float32)
+    p = tmp_path / "tone.aiff"
+    _write_stdlib(aifc, p, x, sr, 2)
+    pipe = AudioToImageInference.__new__(AudioToImageInference)
+    a = pipe.load_audio(str(p), duration=10)
+    assert a.shape == (10 * SR,) and abs(np.abs(a).max() - 1.0) < 1e-6
+    spec = np.abs(np.fft.rfft(a[SR:3 * SR]))
+    assert abs(np.argmax(spec) * SR / (2 * SR) - 1000.0) < 1.0
+    q = tmp_path / "x.mp3"
+    q.write_bytes(b"ID3\x03\x00" + bytes(100))
+    with pytest.raises(ValueError, match="AIFF/AIFC or Sun AU"):
+        read_audio(str(q))
