@@ -68,8 +68,8 @@ def _read_wav(path: str, max_seconds: float | None = None) -> tuple[np.ndarray, 
     """RIFF/WAVE reader -> (mono float32 in [-1, 1], native rate): PCM 8 (unsigned) / 16 / 24 / 32-bit,
     IEEE float 32 / 64-bit, WAVE_FORMAT_EXTENSIBLE of either; channels averaged (librosa mono=True).
     max_seconds: keep the first max_seconds of the file at its native rate (librosa's duration=,
-    applied before resampling as librosa.load does).  Other containers (mp3, flac, ...) need a
-    decoder this image does not have: convert them to WAV first."""
+    applied before resampling as librosa.load does).  read_audio adds AIFF / AIFC and Sun AU; other
+    containers (mp3, flac, ...) need a decoder this image does not have: convert them first."""
     data = Path(path).read_bytes()
     if data[:4] != b"RIFF" or data[8:12] != b"WAVE":
         raise ValueError(f"{path}: not a RIFF/WAVE file (only WAV is decoded without librosa)")
