@@ -101,7 +101,10 @@ int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
 
 /*
  * Bytes of split-K workspace c2d_conv2d_igemm would use for this descriptor
- * (0 = the shape fills the chip without splitting K; sized for fp32 partials).
+ * (0 = the shape fills the chip without splitting K; sized for fp32 partials).  A one-slice
+ * plan can still ask for some: when its grid is whole rounds of the chip plus at most a quarter
+ * round (c5's level-0 convs: 288 tiles on 256 CUs), the last images run as a second launch on
+ * their own plan, which may split K (c2d_conv2d_igemm_plan reports the first launch's plan).
  * Under-filled GEMMs (the 16x16 / 8x8 UNet levels: 80-160 output tiles on 256 CUs)
  * split K across blocks into [split][m][cout] slabs of partial sums that a second,
  * stream-ordered kernel adds in fp32 in fixed order before the epilogue
