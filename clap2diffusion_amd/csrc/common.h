@@ -54,7 +54,7 @@ extern thread_local int g_last_hip_error;
 struct Tuning {
     int gemm_mode, gemm_korder, gemm_lds_epi, gemm_abl, splitk_f16, tail_split;
     int attn_negc, attn_res, attn_w8, attn_pp, attn_abl;
-    int gn_blocks, gn_apply_blocks, gn_fused_hw, gn_fold, gn_fold_cap;
+    int gn_blocks, gn_apply_blocks, gn_fused_hw, gn_fold, gn_fold_cap, gn_fold_apply_blocks;
 };
 const Tuning& tuning();
 // c2d_set_plan_override (tests / sweeps): 0 = the planner decides

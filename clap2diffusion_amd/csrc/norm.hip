@@ -864,7 +864,9 @@ static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n
     }
     const int L = nch < 256 ? nch : 256, R = 256 / L;
     const int npix = pw ? (hw / (pw - 2) + 2) * pw : hw;
-    int bx = (gn_apply_blocks() + n - 1) / n;
+    // fewer, longer apply workgroups than the three-launch apply: each one folds the pairs first
+    // (1024 vs 2048: c2's norms 1-2 us faster, c3's equal; profiles/r04_gn_two_launch_ab.txt)
+    int bx = (tuning().gn_fold_apply_blocks + n - 1) / n;
     const int maxb = (npix + R - 1) / R;
     if (bx > maxb) bx = maxb;
     if (bx < 1) bx = 1;
