@@ -864,9 +864,10 @@ static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n
     }
     const int L = nch < 256 ? nch : 256, R = 256 / L;
     const int npix = pw ? (hw / (pw - 2) + 2) * pw : hw;
-    // fewer, longer apply workgroups than the three-launch apply: each one folds the pairs first
-    // (1024 vs 2048: c2's norms 1-2 us faster, c3's equal; profiles/r04_gn_two_launch_ab.txt)
-    int bx = (tuning().gn_fold_apply_blocks + n - 1) / n;
+    // small batches: fewer, longer apply workgroups (each folds the pairs first): 1024 vs 2048 made
+    // c2's norms 1-2 us faster and c2 0.3079 -> 0.3065 s; c3's N = 16 keeps 2048 (equal per call, the
+    // bench 0.1-0.2 % either way; profiles/r04_gn_two_launch_ab.txt)
+    int bx = ((n < 8 ? tuning().gn_fold_apply_blocks : gn_apply_blocks()) + n - 1) / n;
     const int maxb = (npix + R - 1) / R;
     if (bx > maxb) bx = maxb;
     if (bx < 1) bx = 1;

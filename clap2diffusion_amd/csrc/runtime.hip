@@ -42,7 +42,7 @@ const Tuning& tuning() {
         t.gn_fold = env_int("C2D_GN_FOLD", 1);   // 0: partial + finalize + apply (A/B)
         t.gn_fold_cap = env_int("C2D_GN_FOLD_CAP", 32);   // most partial blocks per image on the fold path
         if (t.gn_fold_cap < 1) t.gn_fold_cap = 32;
-        t.gn_fold_apply_blocks = env_int("C2D_GN_FOLD_APPLY_BLOCKS", 1024);   // apply workgroups per launch (fold path)
+        t.gn_fold_apply_blocks = env_int("C2D_GN_FOLD_APPLY_BLOCKS", 1024);   // apply workgroups per launch (fold path, batches below 8 images)
         if (t.gn_fold_apply_blocks < 64) t.gn_fold_apply_blocks = 1024;
 #ifdef C2D_ENABLE_ABLATION
         t.gemm_abl = env_int("C2D_GEMM_ABL", 0);
