@@ -744,6 +744,7 @@ void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #include "igemm_pp16.h"
 #include "igemm_pps.h"
 #include "igemm_pp16r.h"
+#include "igemm_sp.h"
 namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -793,12 +794,25 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
-C2D_TILE_FN(42);
+C2D_TILE_FN(42); C2D_TILE_FN(60); C2D_TILE_FN(61); C2D_TILE_FN(62); C2D_TILE_FN(63);
 #if C2D_PART(1)
+#ifdef C2D_SP_STAMP
+}  // namespace c2d
+// diagnostic variant only (not in c2d.h): copy the stamps of the last stamped launch to host memory
+extern "C" int c2d_debug_sp_stamps(unsigned long long* host, int n) {
+    if (n > 8 * c2d::kStampPer) n = 8 * c2d::kStampPer;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(c2d::g_sp_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -4;
+}
+namespace c2d {
+#endif
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
 C2D_TILE_FN(50) { (void)ksize; (void)cout; run_pps(p, s); }   // persistent 192x256, carried epilogue (1x1)
 C2D_TILE_FN(42) { (void)ksize; (void)cout; run_pp16r<5>(p, s); }   // 256x320 row-ring 3x3 over a zero-bordered source
+C2D_TILE_FN(60) { run_sp<5, 0>(p, ksize, cout, s); }   // 256x320 software-pipelined, one barrier per K step
+C2D_TILE_FN(61) { run_sp<4, 0>(p, ksize, cout, s); }   // 256x256 software-pipelined
+C2D_TILE_FN(62) { run_sp<5, 3>(p, ksize, cout, s); }   // 60 with the SIMD partners' DMA staggered
+C2D_TILE_FN(63) { run_sp<4, 3>(p, ksize, cout, s); }   // 61 staggered
 #endif
 #if C2D_PART(2)
 C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
@@ -841,6 +855,11 @@ static const DmaTile kDmaTiles[] = {
     {9, 64, 160, 2, 0.0f, false},
     // row-ring 3x3 over a zero-bordered source (igemm_pp16r.h): chosen by plan_for only
     {42, 256, 320, 1, 0.0f, false},
+    // software-pipelined twins of 40 / 41 (igemm_sp.h): one barrier per K step
+    {60, 256, 320, 1, 0.0f, false},
+    {61, 256, 256, 1, 0.0f, true},
+    {62, 256, 320, 1, 0.0f, false},
+    {63, 256, 256, 1, 0.0f, true},
 };
 struct DmaPlan { int id, split, nkt; };
 
@@ -1064,7 +1083,14 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
 static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout, hipStream_t s) {
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
-    switch (pl.id) {
+    int id = pl.id;
+    if (tuning().gemm_sp && id == 40) id = 60;   // C2D_GEMM_SP: the software-pipelined twins (A/B)
+    if (tuning().gemm_sp && id == 41) id = 61;
+    switch (id) {
+        case 60: return run_tile_60(p, ksize, cout, s);
+        case 61: return run_tile_61(p, ksize, cout, s);
+        case 62: return run_tile_62(p, ksize, cout, s);
+        case 63: return run_tile_63(p, ksize, cout, s);
         case 42: return run_tile_42(p, ksize, cout, s);
         case 25: return run_tile_25(p, ksize, cout, s);
         case 40: return run_tile_40(p, ksize, cout, s);
@@ -1219,6 +1245,8 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     // zero-bordered source [n][h + 2][w + 2][c0]: 3x3, stride 1, one source, output h x w
     if (d->src_pad && (d->ksize != 3 || d->stride != 1 || d->up || d->c1 || d->oh != d->h || d->ow != d->w))
         return C2D_E_SHAPE;
+    // ... and no prologue: the border is read as data (pad 0), so GN / LN / SiLU would map it to act(shift)
+    if (d->src_pad && d->pro != C2D_PRO_NONE) return C2D_E_ARG;
 
     IgemmParams p;
     p.src0 = (const f16*)d->src0; p.src1 = (const f16*)d->src1;

@@ -39,14 +39,18 @@ __device__ __forceinline__ int lds_sw(int row, int c) {
 // instruction) covers RPP = 1024 / RB rows; the NA + NB pieces of a stage are
 // dealt round-robin to the NW waves, A first (NA % NW == 0, so piece slot i is
 // an A slot for i < NA / NW in every wave; the last B slot may be partial).
-template <int BM, int BN, int BK, int NW, int KS, int SW = 0>
+// PRE: keep each A row's byte offset in both sources (a_off0 / a_off1, 2 x SA VGPRs) instead of
+// its pixel index (a_pix, SA VGPRs), so a piece's address costs a select and an or, not a 64-bit
+// multiply-add (igemm_sp.h issues its pieces inside the MFMA stream)
+template <int BM, int BN, int BK, int NW, int KS, int SW = 0, bool PRE = false>
 struct M32Loader {
     static constexpr int RB = 2 * BK, RPP = 1024 / RB, CPR = BK / 8;
     static constexpr int NA = BM / RPP, NB = BN / RPP;
     static constexpr int SA = NA / NW;
     static constexpr int SB = (NB + NW - 1) / NW;
     static_assert(NA % NW == 0, "A pieces must split evenly over the waves");
-    int a_pix[SA];          // window-origin pixel index (+pshift) of this lane's row in A slot i
+    int a_pix[PRE ? 1 : SA];          // window-origin pixel index (+pshift) of this lane's row in A slot i
+    unsigned a_off0[PRE ? SA : 1], a_off1[PRE ? SA : 1];   // PRE: its byte offsets in source 0 / 1
     unsigned a_mask[SA];    // in-bounds 3x3 taps of that row
     unsigned b_off[SB];
     unsigned bytes0, bytes1, wbytes;
@@ -85,7 +89,14 @@ struct M32Loader {
                         if (iy0 + ky >= 0 && iy0 + ky < p.h && ix0 + kx >= 0 && ix0 + kx < p.w)
                             mask |= 1u << (ky * KS + kx);
             }
-            a_pix[i] = (nn * p.h + iy0) * p.w + ix0 + pshift;
+            const int pix = (nn * p.h + iy0) * p.w + ix0 + pshift;
+            if constexpr (PRE) {
+                const int ch = chunk_of(row_of(wave, i));
+                a_off0[i] = (unsigned)(2 * (pix * p.c0 + ch));
+                a_off1[i] = (unsigned)(2 * (pix * p.c1 + ch));
+            } else {
+                a_pix[i] = pix;
+            }
             a_mask[i] = mask;
         }
 #pragma unroll
@@ -115,9 +126,13 @@ struct M32Loader {
     // per-stage wave-uniform part of the addressing (descriptors in SGPRs)
     struct Stage {
         __amdgpu_buffer_rsrc_t ra, rb;
-        int cs, lim;
+        int cs, lim, tap;   // tap: the 3x3 tap of this stage, for the halo mask of its A pieces
+        bool use1;          // the stage reads source 1 (the skip-concat's second tensor)
     };
-    __device__ __forceinline__ Stage prep(const IgemmParams& p) const {
+    __device__ __forceinline__ Stage prep(const IgemmParams& p) const { return prep_at(p, tap, cbase); }
+    // the stage at an explicit loader position (tap, cbase) -- kernels that deal one K step's
+    // pieces across two loop iterations keep these two ints, not a Stage, across the loop
+    __device__ __forceinline__ Stage prep_at(const IgemmParams& p, int tap, int cbase) const {
         Stage st;
         const int k0 = tap * p.cin + cbase;              // packed weight column of this step
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
@@ -130,6 +145,8 @@ struct M32Loader {
         st.ra = make_rsrc(sb + sterm - bias, sbytes + bias - sterm);
         st.rb = make_rsrc(u_wt + 2 * k0, wbytes - 2 * k0);
         st.lim = p.cin - cbase;
+        st.tap = tap;
+        st.use1 = use1;
         return st;
     }
     // DMA piece i (< PMAX; A slots first) of this wave into the stage image at lds;
@@ -138,9 +155,11 @@ struct M32Loader {
         if (i < SA) {
             const int ch = chunk_of(row_of(wave, i));
             // branch-free: a dropped tap / channel tail pushes the offset past num_records
-            unsigned ok = (a_mask[i] >> tap) & 1u;
+            unsigned ok = (a_mask[i] >> st.tap) & 1u;   // the stage's tap: the loader may have advanced
             if (ctail) ok &= (unsigned)(ch < st.lim);
-            const unsigned off = (unsigned)(2 * (a_pix[i] * st.cs + ch)) | ((ok - 1u) & kOOB);
+            unsigned off;
+            if constexpr (PRE) off = (st.use1 ? a_off1[i] : a_off0[i]) | ((ok - 1u) & kOOB);
+            else off = (unsigned)(2 * (a_pix[i] * st.cs + ch)) | ((ok - 1u) & kOOB);
             dma_piece(st.ra, lds + (wave + i * NW) * 1024, off);
         } else {
             const int j = i - SA;

@@ -845,7 +845,15 @@ static bool gn_use_fused(int n, int cin, int hw, int groups) {
 
 // partial (per-group pairs) + apply-with-fold: two launches where c2d_groupnorm_stats +
 // c2d_groupnorm_apply take three (C2D_GN_FOLD=0 restores those, A/B only).  Needs groups <= 256.
-static bool gn_use_fold(int cin, int groups) { return tuning().gn_fold != 0 && groups <= 256 && (cin >> 3) <= 512; }
+// Every apply workgroup folds all its image's partial pairs (nblk x groups x 8 B), so the fold pays
+// only while partial blocks stay near the cap: rows per block stop at 128, which leaves a 512^2 VAE
+// image 2048 blocks (512 KB of L2 reads per apply workgroup); past 4 x cap blocks (32 KB at 32
+// groups: c5's 96^2 UNet norms at 72 fold, the VAE's 256^2 / 512^2 norms do not) the stats kernel's
+// parallel finalize + the plain apply run instead.
+static bool gn_use_fold(int n, int cin, int hw, int groups) {
+    return tuning().gn_fold != 0 && groups <= 256 && (cin >> 3) <= 512 &&
+           gn_blocks(n, cin, hw, tuning().gn_fold_cap) <= 4 * tuning().gn_fold_cap;
+}
 
 static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n, int hw, int pw, int groups,
                        float eps, const float* gamma, const float* beta, int silu, void* out, void* ws, hipStream_t s) {
@@ -914,7 +922,7 @@ extern "C" int c2d_groupnorm(const void* src0, const void* src1, int c0, int c1,
         return check_launch();
     }
     if (!ws || ws_bytes < c2d_groupnorm_run_workspace_size(n, cin, hw, groups) || !aligned16(ws)) return C2D_E_ARG;
-    if (gn_use_fold(cin, groups))   // ws sized for the group pairs too (gn_fold_ws_bytes)
+    if (gn_use_fold(n, cin, hw, groups))   // ws sized for the group pairs too (gn_fold_ws_bytes)
         return gn_fold_run(src0, src1, c0, c1, n, hw, 0, groups, eps, gamma, beta, silu, out, ws, s);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);
     float* scale = reinterpret_cast<float*>(static_cast<char*>(ws) + part);
@@ -942,7 +950,7 @@ extern "C" int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int
     if (!aligned16(src0) || (src1 && !aligned16(src1)) || !aligned16(out) || !aligned16(ws)) return C2D_E_ALIGN;
     const int hw = h * w;
     if (ws_bytes < c2d_groupnorm_pad_workspace_size(n, cin, h, w)) return C2D_E_ARG;
-    if (gn_use_fold(cin, groups))
+    if (gn_use_fold(n, cin, hw, groups))
         return gn_fold_run(src0, src1, c0, c1, n, hw, w + 2, groups, eps, gamma, beta, silu, out, ws,
                            (hipStream_t)stream);
     const size_t part = c2d_groupnorm_workspace_size(n, cin, hw);

@@ -98,6 +98,8 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
         _, h, w, _ = x.shape
         if padded:
             assert ksize == 3 and stride == 1 and not up and x2 is None, "padded source: 3x3, stride 1, one source"
+            # the zero border is data to the kernels (pad 0): a prologue would map it to shift / SiLU(shift)
+            assert gn is None and ln is None and not silu_in, "padded source: no GN / LN / SiLU prologue"
             h, w = h - 2, w - 2
     assert x.is_contiguous() and x.dtype == F16
     if x2 is not None:
@@ -135,6 +137,17 @@ def rowring_conv(n: int, h: int, w: int, cin: int, cout: int) -> bool:
     tid, ks = ctypes.c_int(), ctypes.c_int()
     check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
     return tid.value == 42
+
+
+def conv_workspace_bytes(n: int, h: int, w: int, c0: int, c1: int, cout: int, ksize: int) -> int:
+    """Split-K workspace c2d_conv2d_igemm asks for on a stride-1 conv (n x h x w, c0 [+ c1] -> cout),
+    as torch_ops.conv2d_igemm allocates it (c2d_conv2d_igemm_workspace_size)."""
+    import ctypes
+    from ._lib import ConvDesc, lib
+    d = ConvDesc()
+    d.c0, d.c1, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = c0, c1, n, h, w, h, w, ksize, 1
+    d.cout, d.kpad, d.out_ld = cout, kpad_of(ksize * ksize * (c0 + c1)), cout
+    return int(lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d)))
 
 
 class record_conv_plans:

@@ -94,7 +94,10 @@ typedef struct c2d_conv_desc {
     size_t ws_bytes;         /* its size; below c2d_conv2d_igemm_workspace_size(): no split */
     int src_pad;             /* 1: src0 is zero-bordered, [n][h+2][w+2][c0] (c2d_groupnorm_pad):
                                 3x3, stride 1, one source, output h x w; tile 42 (the row-ring
-                                conv) runs it at w = 64, every other tile as a valid 3x3     */
+                                conv) runs it at w = 64, every other tile as a valid 3x3.
+                                No prologue (pro must be C2D_PRO_NONE, else C2D_E_ARG): the
+                                border is read as data, so a GN / LN / SiLU would turn it into
+                                act(shift) instead of the zero padding torch applies        */
 } c2d_conv_desc;
 
 int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);

@@ -4,7 +4,7 @@
 # MFMA, LDS, VALU + L2, FETCH_SIZE, WRITE_SIZE), summarised per shape into gpurun_out/gemmpmc/.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-D=gpurun_out/gemmpmc; mkdir -p $D
+D=gpurun_out/gemmpmc${TAG}; mkdir -p $D   # TAG: a suffix per run (e.g. the forced tile, C2D_GEMM_TILE)
 G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT"
 G2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INSTS_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS"
 G3="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum"

@@ -102,6 +102,16 @@ int main() {
         d.src_pad = 1;   // a padded source is stride 1 only
         CHECK(c2d_conv2d_igemm(&d, nullptr) == C2D_E_SHAPE);
     }
+    {
+        // a padded source takes no prologue: its zero border would become act(shift)
+        static float tab[16 * 320];
+        c2d_conv_desc d = desc(16, 64, 64, 320, 0, 3, 1, 320, C2D_ACT_NONE);
+        d.src_pad = 1;
+        d.pro = C2D_PRO_GN; d.pro_a = tab; d.pro_b = tab;
+        CHECK(c2d_conv2d_igemm(&d, nullptr) == C2D_E_ARG);
+        d.pro = C2D_PRO_SILU; d.pro_a = nullptr; d.pro_b = nullptr;
+        CHECK(c2d_conv2d_igemm(&d, nullptr) == C2D_E_ARG);
+    }
     for (int nb : {1, 2, 8})                                            // VAE decoder
         for (int hw : {64, 128, 256, 512})
             for (int c : {128, 256, 512}) check_plan(desc(nb, hw, hw, c, 0, 3, 1, c, C2D_ACT_NONE));

@@ -144,7 +144,7 @@ def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
 
 # every tile configuration left in igemm.hip's kDmaTiles, forced through
 # c2d_set_plan_override and confirmed through c2d_conv2d_igemm_plan
-DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3, 8, 9]
+DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3, 8, 9, 60, 61, 62, 63]
 
 
 @pytest.mark.parametrize("tile", DMA_TILE_IDS)
@@ -351,7 +351,7 @@ def test_epilogue_operand_forms(dev, force_plan, tile, cout, temb, resid, bias):
     close(nchw(out), ref)
 
 
-@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 8, 9, 40)])   # odd column tiles: no GEGLU
+@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 8, 9, 40, 60, 62)])   # odd column tiles: no GEGLU
 def test_every_dma_tile_forced_geglu(dev, force_plan, tile):
     m, cin, inner = 1024, 320, 640
     force_plan(tile, 1)
@@ -825,6 +825,8 @@ def test_conv_quantisation_tail(dev, c0, c1, res, tmb, padded):
             x0, x1 = (xd[..., :c0].contiguous(), xd[..., c0:].contiguous()) if c1 else (xd, None)
             out = ops.conv(x0, wp.to(dev), kp, cout, ksize=3, x2=x1, **kw)
     assert plans == [(40, 1)], plans
+    if c1:   # the tail image's own plan splits K 3 ways into the workspace the call allocated
+        assert ops.conv_workspace_bytes(n, h, h, c0, c1, cout, 3) == 3 * h * h * cout * 4
     close(nchw(out), ref)
 
 

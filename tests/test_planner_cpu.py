@@ -7,13 +7,13 @@ import ctypes
 import pytest
 
 
-def _plan(cin, cout, n, h, k, ws=True, geglu=False):
+def _plan(cin, cout, n, h, k, ws=True, geglu=False, c1=0):
     import torch  # noqa: F401  (binds the library to torch's HIP runtime first)
     from clap2diffusion_amd import _lib, ops
     L = _lib.lib()
     d = _lib.ConvDesc()
-    d.c0, d.c1, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, 0, n, h, h, h, h, k, 1
-    d.cout, d.kpad = cout, ops.kpad_of(k * k * cin)
+    d.c0, d.c1, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, c1, n, h, h, h, h, k, 1
+    d.cout, d.kpad = cout, ops.kpad_of(k * k * (cin + c1))
     if geglu:
         d.act = 1   # C2D_ACT_GEGLU
     if ws:   # a workspace large enough for any split (the planner only reads the pointer / size)
@@ -51,12 +51,12 @@ def test_table_split_needs_workspace_and_other_shapes_use_the_rules():
 
 
 
-def _ws(cin, cout, n, h, k):
+def _ws(cin, cout, n, h, k, c1=0):
     import torch  # noqa: F401
     from clap2diffusion_amd import _lib, ops
     d = _lib.ConvDesc()
-    d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, n, h, h, h, h, k, 1
-    d.cout, d.kpad = cout, ops.kpad_of(k * k * cin)
+    d.c0, d.c1, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = cin, c1, n, h, h, h, h, k, 1
+    d.cout, d.kpad = cout, ops.kpad_of(k * k * (cin + c1))
     return _lib.lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
 
 
@@ -69,3 +69,14 @@ def test_quantisation_tail_reports_the_head_plan():
     assert _ws(320, 320, 8, 96, 3) == 0
     assert _plan(320, 320, 1, 96, 3) == (3, 1)           # what the tail image runs
     assert _plan(320, 320, 16, 64, 3) == (40, 1) and _ws(320, 320, 16, 64, 3) == 0   # c3: exact fit
+
+
+@pytest.mark.parametrize("c0,c1", [(320, 320), (640, 320)])
+def test_quantisation_tail_split_k_workspace(c0, c1):
+    """The up-block concat convs of c5 (640 / 960 -> 320 at 96^2, 8 images) split the same way, and
+    their tail image plans split-K 3 on the 128 x 320 tile: the workspace the call asks for is
+    exactly the tail's slabs (3 x 9216 rows x 320 x fp32), not the head's (one slice, none).
+    tests/test_kernels_gpu.py::test_conv_quantisation_tail runs these cases on the GPU."""
+    assert _plan(c0, 320, 8, 96, 3, c1=c1) == (40, 1)
+    assert _plan(c0, 320, 1, 96, 3, c1=c1) == (7, 3)
+    assert _ws(c0, 320, 8, 96, 3, c1=c1) == 3 * 9216 * 320 * 4
