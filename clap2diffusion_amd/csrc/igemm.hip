@@ -745,6 +745,7 @@ void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #include "igemm_pps.h"
 #include "igemm_pp16r.h"
 #include "igemm_sp.h"
+#include "igemm_spr.h"
 namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -794,7 +795,7 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
-C2D_TILE_FN(42); C2D_TILE_FN(60); C2D_TILE_FN(61); C2D_TILE_FN(62); C2D_TILE_FN(63);
+C2D_TILE_FN(42); C2D_TILE_FN(60); C2D_TILE_FN(61); C2D_TILE_FN(62);
 #if C2D_PART(1)
 #ifdef C2D_SP_STAMP
 }  // namespace c2d
@@ -809,10 +810,9 @@ C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
 C2D_TILE_FN(50) { (void)ksize; (void)cout; run_pps(p, s); }   // persistent 192x256, carried epilogue (1x1)
 C2D_TILE_FN(42) { (void)ksize; (void)cout; run_pp16r<5>(p, s); }   // 256x320 row-ring 3x3 over a zero-bordered source
-C2D_TILE_FN(60) { run_sp<5, 0>(p, ksize, cout, s); }   // 256x320 software-pipelined, one barrier per K step
-C2D_TILE_FN(61) { run_sp<4, 0>(p, ksize, cout, s); }   // 256x256 software-pipelined
-C2D_TILE_FN(62) { run_sp<5, 3>(p, ksize, cout, s); }   // 60 with the SIMD partners' DMA staggered
-C2D_TILE_FN(63) { run_sp<4, 3>(p, ksize, cout, s); }   // 61 staggered
+C2D_TILE_FN(60) { run_sp<5>(p, ksize, cout, s); }   // 256x320 software-pipelined, two barriers per K step
+C2D_TILE_FN(61) { run_sp<4>(p, ksize, cout, s); }   // 256x256 software-pipelined
+C2D_TILE_FN(62) { (void)ksize; (void)cout; run_spr<5>(p, s); }   // 256x320 row-ring software-pipelined 3x3
 #endif
 #if C2D_PART(2)
 C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
@@ -858,8 +858,7 @@ static const DmaTile kDmaTiles[] = {
     // software-pipelined twins of 40 / 41 (igemm_sp.h): one barrier per K step
     {60, 256, 320, 1, 0.0f, false},
     {61, 256, 256, 1, 0.0f, true},
-    {62, 256, 320, 1, 0.0f, false},
-    {63, 256, 256, 1, 0.0f, true},
+    {62, 256, 320, 1, 0.0f, false},   // row-ring twin of 42 (igemm_spr.h): chosen like 42, never by plan_dma
 };
 struct DmaPlan { int id, split, nkt; };
 
@@ -1006,8 +1005,12 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
     int id = gemm_tile();
-    if (id == 42) {
-        if (rr_ok) return rr_plan(nk, gemm_split());
+    if (id == 42 || id == 62) {
+        if (rr_ok) {
+            DmaPlan pl = rr_plan(nk, gemm_split());
+            pl.id = id;
+            return pl;
+        }
         id = 0;
     }
     // the row-ring 3x3 (tile 42) on a zero-bordered source once its 256 x 320 tiles fill the chip
@@ -1086,11 +1089,11 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     int id = pl.id;
     if (tuning().gemm_sp && id == 40) id = 60;   // C2D_GEMM_SP: the software-pipelined twins (A/B)
     if (tuning().gemm_sp && id == 41) id = 61;
+    if (tuning().gemm_sp && id == 42) id = 62;
     switch (id) {
         case 60: return run_tile_60(p, ksize, cout, s);
         case 61: return run_tile_61(p, ksize, cout, s);
         case 62: return run_tile_62(p, ksize, cout, s);
-        case 63: return run_tile_63(p, ksize, cout, s);
         case 42: return run_tile_42(p, ksize, cout, s);
         case 25: return run_tile_25(p, ksize, cout, s);
         case 40: return run_tile_40(p, ksize, cout, s);

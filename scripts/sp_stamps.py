@@ -1,8 +1,8 @@
 """Per-K-step timeline of the software-pipelined GEMM (tile 60 / 61) from the diagnostic stamp build:
 python -m clap2diffusion_amd.build --variant stamp --define C2D_SP_STAMP, then on the GPU
 C2D_LIB=clap2diffusion_amd/libc2d_hip_stamp.so python scripts/sp_stamps.py --shape conv0 --tile 60
-Prints, per wave of workgroup 77 (s_memtime cycles): prologue, per-step compute (group 0 -> 13),
-the vmcnt / lgkmcnt drain before the barrier, the barrier wait, and the epilogue."""
+Prints, per wave of workgroup 77 (s_memtime cycles): prologue, per step groups 0-10, the vmcnt drain +
+barrier X1, groups 11-13 + barrier X2, groups 14-15 + the next step's top wait, and the epilogue."""
 import argparse
 import ctypes
 import statistics
@@ -27,24 +27,22 @@ with ops.force_plan(a.tile, a.split):
     for _ in range(20):
         ab_tiles.call(c)
 torch.cuda.synchronize()
-PER = 4 * 64 + 4
+PER = 6 * 64 + 4
 buf = (ctypes.c_ulonglong * (8 * PER))()
 assert _lib.lib().c2d_debug_sp_stamps(buf, 8 * PER) == 0
+names = ["g0-10", "X1", "g11-13+X2", "g14", "g15", "top wait"]
 for w in range(8):
     t = [buf[w * PER + i] for i in range(PER)]
     t0 = t[0]
-    steps = []
+    rows = []
     k = 0
-    while 7 + 4 * k < PER and t[7 + 4 * k] > t0:
-        s0, s1, s2, s3 = t[4 + 4 * k], t[5 + 4 * k], t[6 + 4 * k], t[7 + 4 * k]
-        steps.append((s1 - s0, s2 - s1, s3 - s2))
+    while 10 + 6 * (k + 1) < PER and t[4 + 6 * (k + 1)] > t0:
+        b0 = 4 + 6 * k
+        s_ = [t[b0 + j] for j in range(6)] + [t[b0 + 6]]
+        rows.append([s_[j + 1] - s_[j] for j in range(6)])
         k += 1
-    if not steps:
+    if not rows:
         continue
-    nxt = [t[4 + 4 * (i + 1)] - t[7 + 4 * i] for i in range(len(steps) - 1)]
-    comp = [x[0] for x in steps]
-    drain = [x[1] for x in steps]
-    bar = [x[2] for x in steps]
-    print(f"wave {w}: steps {len(steps)}  prologue {t[1] - t0}  loop {t[2] - t[1]}  epilogue {t[3] - t[2]}  | per step: "
-          f"g0-13 {statistics.median(comp):.0f}  drain {statistics.median(drain):.0f}  barrier {statistics.median(bar):.0f}  "
-          f"g14-15 {statistics.median(nxt) if nxt else 0:.0f}  (max g0-13 {max(comp)}, max barrier {max(bar)})")
+    med = [statistics.median(r[j] for r in rows) for j in range(6)]
+    print(f"wave {w}: steps {len(rows) + 1}  prologue {t[1] - t0}  loop {t[2] - t[1]}  epilogue {t[3] - t[2]}  | per step: " +
+          "  ".join(f"{n} {m:.0f}" for n, m in zip(names, med)) + f"  (sum {sum(med):.0f})")
