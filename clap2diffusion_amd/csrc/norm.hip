@@ -845,14 +845,15 @@ static bool gn_use_fused(int n, int cin, int hw, int groups) {
 
 // partial (per-group pairs) + apply-with-fold: two launches where c2d_groupnorm_stats +
 // c2d_groupnorm_apply take three (C2D_GN_FOLD=0 restores those, A/B only).  Needs groups <= 256.
-// Every apply workgroup folds all its image's partial pairs (nblk x groups x 8 B), so the fold pays
-// only while partial blocks stay near the cap: rows per block stop at 128, which leaves a 512^2 VAE
-// image 2048 blocks (512 KB of L2 reads per apply workgroup); past 4 x cap blocks (32 KB at 32
-// groups: c5's 96^2 UNet norms at 72 fold, the VAE's 256^2 / 512^2 norms do not) the stats kernel's
-// parallel finalize + the plain apply run instead.
+// Every apply workgroup folds all its image's partial pairs (nblk x groups x 8 B).  Rows per
+// partial block stop at 128, so a 512^2 VAE image has 2048 blocks (512 KB of L2 reads per apply
+// workgroup at 32 groups); measured against the three-launch path (parallel finalize +
+// plain apply) on the VAE shapes at 8 images the fold is still faster -- 256^2 x 512 318.8 vs
+// 336.3 us, 512^2 x 256 644.1 vs 698.1 us, 512^2 x 128 356.9 vs 392.1 us, graph-replayed on one box
+// (profiles/r05_gn_vae_fold_ab.txt) -- so every shape within the kernel's limits folds.
 static bool gn_use_fold(int n, int cin, int hw, int groups) {
-    return tuning().gn_fold != 0 && groups <= 256 && (cin >> 3) <= 512 &&
-           gn_blocks(n, cin, hw, tuning().gn_fold_cap) <= 4 * tuning().gn_fold_cap;
+    (void)n; (void)hw;
+    return tuning().gn_fold != 0 && groups <= 256 && (cin >> 3) <= 512;
 }
 
 static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n, int hw, int pw, int groups,

@@ -14,6 +14,8 @@ N = int(os.environ.get("GN_N", "16"))
 SHAPES = [(64, 320, 0), (64, 320, 320), (64, 640, 320), (32, 640, 0), (32, 640, 320), (32, 640, 640), (32, 1280, 640),
           (16, 1280, 0), (16, 1280, 1280),
           (8, 1280, 0), (8, 1280, 1280)]
+if os.environ.get("GN_SHAPES") == "vae":   # the VAE decoder's GroupNorms (GN_N=8: c3's batch)
+    SHAPES = [(64, 512, 0), (128, 512, 0), (256, 512, 0), (256, 256, 0), (512, 256, 0), (512, 128, 0)]
 REPS = 20
 for h, c0, c1 in SHAPES:
     x = torch.randn(N, h, h, c0, device=dev, dtype=torch.float16) * 2 + 0.5
