@@ -81,6 +81,26 @@ def measure_dominant_kernel(dev, iters: int = 20):
             "flop_per_launch": flop, "avg_us": round(ms * 1e3, 2)}
 
 
+def family_fractions(den):
+    """roofline.family_frac: per kernel family of one denoise step of the benchmarked batch, the
+    family's algorithmic work over its time -- FLOP / (time x 2.5 PF/s) for the MFMA families,
+    bytes / (time x 8 TB/s) for the HBM ones -- with every c2d call of the step recorded and each
+    unique call timed as a graph of back-to-back replays (scripts/ledger.py, whose full per-shape
+    table for c3 / c2 is profiles/r05_ledger_*.txt)."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from ledger import step_ledger
+    rows, fams, meta = step_ledger(den)
+    out = {}
+    for f, s in fams.items():
+        out[f] = round(s["mfma_frac"] if s["flop"] > 0 else s["frac"], 4)
+    return out, {"ledger_ms_per_step": round(fams["all"]["us"] / 1e3, 3),
+                 "step_graph_ms": None if meta["step_us"] is None else round(meta["step_us"] / 1e3, 3),
+                 "family_ms_per_step": {f: round(s["us"] / 1e3, 3) for f, s in fams.items()},
+                 "family_source": "scripts/ledger.py step_ledger: every c2d call of one denoise step, each unique "
+                                  "call timed as a graph of 10 back-to-back replays; FLOP / (t x 2.5 PF/s) for "
+                                  "families with FLOP, bytes / (t x 8 TB/s) for norms and elementwise"}
+
+
 def pmc_traffic(timeout_s: int = 120):
     """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters, one
     counter per pass (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE (KiB, reported
@@ -254,6 +274,11 @@ def main():
         n_, h_, c_ = 16, 64, 320
         # padded x + resid + out + weights
         roof["algorithmic_bytes"] = 2 * (n_ * (h_ + 2) ** 2 * c_ + 2 * n_ * h_ * h_ * c_ + c_ * 9 * c_)
+        try:
+            roof["family_frac"], fam_meta = family_fractions(pipe.last_denoiser)
+            roof.update(fam_meta)
+        except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench
+            roof["family_frac"], roof["family_source"] = None, f"ledger failed: {type(e).__name__}: {e}"
         if not a.no_pmc and ctx.world == 1:
             tr, src = pmc_traffic()
             roof["traffic"] = None if tr is None else round(tr)

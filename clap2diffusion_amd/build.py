@@ -62,7 +62,7 @@ def _compile(unit, build_dir: Path, defines=(), flags=()) -> Path:
 def build(force: bool = False, jobs: int = 4, verbose: bool = True, ablation: bool = False,
           variant: str = "", variant_defines: tuple = (), variant_flags: tuple = ()) -> Path:
     """ablation=True builds libc2d_hip_abl.so with -DC2D_ENABLE_ABLATION (timing-ablation
-    switches live; wrong results by design) for scripts/gpu_gemm_abl.sh via C2D_LIB; the
+    switches live; wrong results by design) for scripts/gpu_abl_tiles.sh via C2D_LIB; the
     production libc2d_hip.so never contains them.  variant="x" with variant_defines builds
     libc2d_hip_x.so (compile-time A/B candidates, loaded through C2D_LIB)."""
     defines = ("C2D_ENABLE_ABLATION",) if ablation else tuple(variant_defines)

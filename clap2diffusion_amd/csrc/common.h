@@ -24,7 +24,7 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Timing-ablation switches (C2D_GEMM_ABL / C2D_ATTN_ABL: skip the DMA, the MFMAs or
 // the epilogue to attribute kernel time; wrong results by design) exist only in a
-// bench build compiled with -DC2D_ENABLE_ABLATION (scripts/gpu_gemm_abl.sh).  In the
+// bench build compiled with -DC2D_ENABLE_ABLATION (scripts/gpu_abl_tiles.sh).  In the
 // production library every ablation test folds to a constant 0 and the environment
 // variables are never read.
 #ifdef C2D_ENABLE_ABLATION

@@ -917,7 +917,7 @@ static bool epi_direct_ok(const c2d_conv_desc* d) {
 static int gemm_split() { return plan_override_split(); }
 
 // Tile choice.  Measured on gfx950 over the UNet's conv / linear shapes
-// (scripts/bench_gemm.py, scripts/sweep_tiles.sh): the 256x320 32x32-MFMA tile
+// (scripts/bench_gemm.py, scripts/sweep_tiles_graph.py): the 256x320 32x32-MFMA tile
 // (id 23) is fastest whenever its tiles fill the chip by themselves (all level-0
 // GEMMs, the GEGLU projections, the 256-row-tile-rich up-block convs); otherwise
 // the 128x320 tile (id 7; GEGLU: 256x128, id 1) when its tiles fill the chip;
@@ -1044,7 +1044,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
         DmaPlan pl = plan_dma(M, cout, nk, geglu, 29, 0);
         if (pl.id == 29) return pl;
     }
-    // rules from the shape sweeps (scripts/sweep_tiles.sh): the 256x320 interleaved-DMA
+    // rules from the shape sweeps (scripts/sweep_tiles_graph.py): the 256x320 interleaved-DMA
     // tile once it (nearly) fills the chip, and with split-K for the long-K convs
     // (9 * cin >= 5760: L1 / L2 resnet and up-block convs); 128x320 below that
     // VAE widths (128 / 256 / 512 channels) leave 320-wide tiles 20-60 % empty: the
@@ -1056,7 +1056,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
         if (cout % 256 != 0 && cout % 128 == 0 && mt * (cout / 128) >= 192) return {29, 1, nk};
     }
     // 256x320: the ping-pong 16x16x32 kernel (tile 40, 5-12 % faster than the 32x32x16
-    // tile 25 on every conv / K >= 320 GEMM shape measured, scripts/gpu_tile_ab.sh) except
+    // tile 25 on every conv / K >= 320 GEMM shape measured, scripts/ab_tiles.py) except
     // for GEGLU, whose [16 h | 16 g] column pairs need 32-aligned per-wave column tiles in
     // the plain (per-wave image) epilogue
     const int t256x320 = (geglu || !C2D_PP16_DEFAULT) ? 25 : 40;

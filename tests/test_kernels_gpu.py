@@ -492,7 +492,7 @@ def test_geglu(dev):
 
 
 # shapes large enough for the planner's 256x320 tile (>= 192 output tiles), its
-# epilogue variants (scripts/gpu_epi_ab.sh runs these with C2D_GEMM_LDSEPI=0 and 1);
+# epilogue variants (scripts/gpu_ab.sh PYTEST_K arms run these with C2D_GEMM_LDSEPI=0 and 1);
 # torch fp32 on the device is the reference
 def test_m32_direct_epilogue_geglu(dev):
     m, c = 16384, 320
