@@ -23,7 +23,7 @@ ARCH = "gfx950"
 SOURCES = ["igemm.hip", "norm.hip", "attention.hip", "elementwise.hip", "audio.hip", "runtime.hip"]
 # compile units: igemm.hip once per kernel family (C2D_IGEMM_PART, see its header) so
 # the families build in parallel; (source, extra defines, object stem)
-UNITS = [("igemm.hip", (f"C2D_IGEMM_PART={k}",), f"igemm_p{k}") for k in range(4)] + \
+UNITS = [("igemm.hip", (f"C2D_IGEMM_PART={k}",), f"igemm_p{k}") for k in range(5)] + \
         [(s, (), Path(s).stem) for s in SOURCES[1:]]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I", str(ROOT / "include")]

@@ -26,7 +26,7 @@
 // The library compiles this file once per kernel family (build.py: -DC2D_IGEMM_PART=k)
 // so the families build in parallel: 0 = host API, planner, register-staged kernels and
 // the split-K combine; 1 = ping-pong 16x16x32 tiles; 2 = 32x32x16 tiles; 3 = 16x16x32
-// LDS-DMA tiles.  Undefined (-1) = everything in one object.
+// LDS-DMA tiles; 4 = the panel GEMM.  Undefined (-1) = everything in one object.
 #ifndef C2D_IGEMM_PART
 #define C2D_IGEMM_PART -1
 #endif
@@ -746,6 +746,7 @@ void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #include "igemm_pp16r.h"
 #include "igemm_sp.h"
 #include "igemm_spr.h"
+#include "igemm_panel.h"
 namespace c2d {
 
 template <int WM, int WN, int TM, int TN, int STAGES, int KS>
@@ -795,7 +796,7 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
-C2D_TILE_FN(42); C2D_TILE_FN(60); C2D_TILE_FN(61); C2D_TILE_FN(62);
+C2D_TILE_FN(42); C2D_TILE_FN(60); C2D_TILE_FN(61); C2D_TILE_FN(62); C2D_TILE_FN(70);
 #if C2D_PART(1)
 #ifdef C2D_SP_STAMP
 }  // namespace c2d
@@ -826,6 +827,9 @@ C2D_TILE_FN(2) { run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s); }   // 128x128, 4 wa
 C2D_TILE_FN(3) { run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s); }   // 64x64, 4 waves of 32x32
 C2D_TILE_FN(8) { run_dma<2, 2, 4, 5, 2>(p, ksize, cout, s); }   // 128x160, 4 waves of 64x80, 72 KiB: 2 per CU
 C2D_TILE_FN(9) { run_dma<2, 2, 2, 5, 2>(p, ksize, cout, s); }   // 64x160, 4 waves of 32x80, 56 KiB: 2 per CU
+#endif
+#if C2D_PART(4)
+C2D_TILE_FN(70) { (void)ksize; (void)cout; run_panel(p, s); }   // 128-row A panel in LDS, weights streamed per wave
 #endif
 }  // namespace c2d
 #undef C2D_TILE_FN
@@ -1001,10 +1005,15 @@ static DmaPlan rr_plan(int nk, int split) {
     return {42, (ncb + cbs - 1) / cbs, 9 * cbs};
 }
 
-static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize, bool rr_ok = false) {
+static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize, bool rr_ok = false,
+                        bool panel_ok = false) {
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
     int id = gemm_tile();
+    if (id == 70) {   // the panel GEMM (igemm_panel.h): one slice, no split
+        if (panel_ok && gemm_split() <= 1) return {70, 1, nk};
+        id = 0;
+    }
     if (id == 42 || id == 62) {
         if (rr_ok) {
             DmaPlan pl = rr_plan(nk, gemm_split());
@@ -1106,6 +1115,7 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 2: return run_tile_2(p, ksize, cout, s);
         case 8: return run_tile_8(p, ksize, cout, s);
         case 9: return run_tile_9(p, ksize, cout, s);
+        case 70: return run_tile_70(p, ksize, cout, s);
         default: return run_tile_3(p, ksize, cout, s);
     }
 }
@@ -1119,6 +1129,15 @@ static bool dma_eligible(const c2d_conv_desc* d) {
     return (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && gemm_mode() != 2 &&
            (d->c1 == 0 || (d->c0 & 63) == 0) && src_bytes < (1u << 31) &&
            (size_t)d->cout * d->kpad * 2 < (1u << 31);  // 32-bit buffer offsets
+}
+
+// the panel GEMM (tile 70, igemm_panel.h): 1x1, one source of 320 / 640 channels, K unpadded,
+// 32-column blocks, no prologue / time embedding, act none or GEGLU (no residual), the direct
+// epilogue's alignment
+static bool panel_eligible(const c2d_conv_desc* d) {
+    return d->ksize == 1 && d->c1 == 0 && (d->c0 == 320 || d->c0 == 640) && d->kpad == d->c0 && (d->cout & 31) == 0 &&
+           d->pro == C2D_PRO_NONE && !d->temb && (d->act == C2D_ACT_NONE || (d->act == C2D_ACT_GEGLU && !d->resid)) &&
+           epi_direct_ok(d) && dma_eligible(d) && (size_t)d->n * d->oh * d->ow * d->out_ld * 2 < (1u << 31);
 }
 
 // the row-ring tile 42 (igemm_pp16r.h) applies to this descriptor
@@ -1168,7 +1187,7 @@ static c2d_conv_desc tail_desc(const c2d_conv_desc* d, int n1) {
 static size_t tail_ws_bytes(const c2d_conv_desc* d, int n1) {
     const c2d_conv_desc t = tail_desc(d, n1);
     const long Mt = (long)t.n * t.oh * t.ow;
-    const DmaPlan tp = plan_for(Mt, t.cout, t.kpad, t.act, pps_eligible(&t), t.ksize, rr_eligible(&t));
+    const DmaPlan tp = plan_for(Mt, t.cout, t.kpad, t.act, pps_eligible(&t), t.ksize, rr_eligible(&t), panel_eligible(&t));
     return tp.split > 1 ? (size_t)tp.split * Mt * t.cout * sizeof(float) : 0;
 }
 
@@ -1176,7 +1195,7 @@ extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
     if (!dma_eligible(d)) return 0;
     const long M = (long)d->n * d->oh * d->ow;
-    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+    const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
     if (const int n1 = tail_images(d, pl)) return tail_ws_bytes(d, n1);
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
@@ -1190,7 +1209,7 @@ extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* 
         return C2D_OK;
     }
     const long M = (long)d->n * d->oh * d->ow;
-    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
     if (pl.split > 1) {
         const size_t need = (size_t)pl.split * M * d->cout * sizeof(float);
         if (!(d->ws && d->ws_bytes >= need && aligned16(d->ws))) pl.split = 1;
@@ -1207,7 +1226,7 @@ extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (d->n >= 2 && d->ksize >= 1 && d->oh > 0 && d->ow > 0 && d->cout > 0 && d->kpad >= 64 && dma_eligible(d)) {
         const long M = (long)d->n * d->oh * d->ow;
-        const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+        const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
         if (const int n1 = tail_images(d, pl)) {   // quantisation tail: whole rounds, then the rest
             c2d_conv_desc head = *d;
             head.n = n1;
@@ -1284,7 +1303,7 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     p.cmajor = gemm_korder();
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
-        DmaPlan pl = fixed ? *fixed : plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d));
+        DmaPlan pl = fixed ? *fixed : plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
         if (pl.split > 1) {
             const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
             if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {

@@ -372,6 +372,58 @@ def test_every_dma_tile_forced_geglu(dev, force_plan, tile):
     close(out, ref)
 
 
+# the panel GEMM (tile 70, igemm_panel.h): K = 320 / 640, 1x1, plain / residual / GEGLU; M not a
+# multiple of the 128-row panel, column blocks not a multiple of the 8 waves, and the column split
+# over several workgroups per panel (small M)
+@pytest.mark.parametrize("m,cin,cout,res", [
+    (4096, 320, 960, False),       # QKV-shaped, 30 column blocks over 8 waves
+    (300, 320, 320, True),         # ragged last panel, column split, residual
+    (2048, 640, 1920, False),      # K = 640 (160 KiB panel), column split
+    (1000, 640, 640, True),
+])
+def test_panel_gemm_forced(dev, force_plan, m, cin, cout, res):
+    force_plan(70, 0)
+    x = gen(m, cin, seed=101)
+    w = gen(cout, cin, seed=102, scale=1.0 / math.sqrt(cin))
+    b = gen(cout, seed=103)
+    r = gen(m, cout, seed=104) if res else None
+    ref = x @ w.t() + b + (r if res else 0)
+    wp, kp = ops.pack_linear_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(x.half().to(dev), wp.to(dev), kp, cout, ksize=1, bias=b.float().to(dev),
+                       resid=r.half().to(dev) if res else None)
+    assert plans == [(70, 1)], plans
+    close(out, ref)
+
+
+@pytest.mark.parametrize("m,cin,inner", [(2048, 320, 1280), (777, 640, 2560)])
+def test_panel_gemm_forced_geglu(dev, force_plan, m, cin, inner):
+    force_plan(70, 0)
+    x = gen(m, cin, seed=105)
+    w = gen(2 * inner, cin, seed=106, scale=1.0 / math.sqrt(cin))
+    b = gen(2 * inner, seed=107)
+    hh, gg = (x @ w.t() + b).chunk(2, -1)
+    ref = hh * F.gelu(gg)
+    wi, bi = ops.geglu_interleave(w, b)
+    wp, kp = ops.pack_linear_weight(wi)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(x.half().to(dev), wp.to(dev), kp, 2 * inner, ksize=1, bias=bi.float().to(dev), act="geglu")
+    assert plans == [(70, 1)], plans
+    close(out, ref)
+
+
+def test_panel_gemm_ineligible_falls_back(dev, force_plan):
+    """Forcing tile 70 on a shape it does not take (K = 1280) leaves the planner's choice."""
+    force_plan(70, 0)
+    x = gen(512, 1280, seed=108)
+    w = gen(640, 1280, seed=109, scale=1.0 / math.sqrt(1280))
+    wp, kp = ops.pack_linear_weight(w)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(x.half().to(dev), wp.to(dev), kp, 640, ksize=1)
+    assert plans and plans[0][0] != 70, plans
+    close(out, x @ w.t())
+
+
 @pytest.mark.parametrize("n,h,c0,c1,cout,k", [
     (2, 8, 1280, 640, 640, 3),      # 64x64 DMA tiles
     (16, 32, 640, 320, 320, 3),     # 128x128 DMA tiles
