@@ -52,7 +52,7 @@ extern thread_local int g_last_hip_error;
 // Tuning switches (A/B only; defaults are the measured best), read from the environment
 // once per process under std::call_once (runtime.hip) and immutable afterwards.
 struct Tuning {
-    int gemm_mode, gemm_korder, gemm_lds_epi, gemm_abl, splitk_f16, tail_split, gemm_sp, panel_regb;
+    int gemm_mode, gemm_korder, gemm_lds_epi, gemm_abl, splitk_f16, tail_split, gemm_sp, panel_regb, panel_stagger;
     int attn_negc, attn_res, attn_w8, attn_pp, attn_abl;
     int gn_blocks, gn_apply_blocks, gn_fused_hw, gn_fold, gn_fold_cap, gn_fold_apply_blocks;
 };

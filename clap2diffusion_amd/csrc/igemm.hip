@@ -975,6 +975,16 @@ static const PlanHint kPlanHints[] = {
     {3, 1152, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 116.7 -> 96.1
     {1, 73728, 1600, 320, false, 7, 1},       // ff.net.2 + proj_out fold L0: 145.6 -> 136.9
     {1, 18432, 3200, 640, false, 41, 1},      // fold L1: 121.9 -> 87.7
+    // the panel GEMM (tile 70, igemm_panel.h), graph-replayed forced sweeps at the three batches
+    // (profiles/r05_panel_gemm.txt); -DC2D_NO_PANEL_HINTS: A/B builds without them
+#ifndef C2D_NO_PANEL_HINTS
+    {1, 65536, 320, 2560, true, 70, 1},       // c3 GEGLU L0: 154.7 -> 120.4 us
+    {1, 16384, 640, 5120, true, 70, 1},       // c3 GEGLU L1: 135.0 -> 117.7
+    {1, 65536, 320, 960, false, 70, 1},       // c3 QKV L0: 68.8 -> 65.2
+    {1, 73728, 320, 2560, true, 70, 1},       // c5 GEGLU L0: 173.8 -> 157.7
+    {1, 8192, 320, 2560, true, 70, 1},        // c2 GEGLU L0: 25.9 -> 20.7
+    {1, 8192, 320, 960, false, 70, 1},        // c2 QKV L0: 13.9 -> 12.5
+#endif
     // N = 16, 64^2 (c3)
     {1, 4096, 1280, 1280, false, 8, 1},       // 1x1 L2: 27.2 -> 24.5
     {1, 1024, 1280, 1280, false, 3, 1},       // 1x1 mid: 18.9 -> 13.5
@@ -1028,7 +1038,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
     if (!id && rr_ok && !gemm_split() && cout % 320 == 0 && (M / 256) * (cout / 320) >= 192) return rr_plan(nk, 1);
     if (!id && !gemm_split()) {   // a forced split (tile left to the planner) skips the table
         DmaPlan pl;
-        if (plan_hint(ksize, M, kpad, cout, geglu, pl) && (pl.id != 50 || pps_ok)) return pl;
+        if (plan_hint(ksize, M, kpad, cout, geglu, pl) && (pl.id != 50 || pps_ok) && (pl.id != 70 || panel_ok)) return pl;
     }
     if (id == 7 && geglu) id = 0;
     if (id == 50) {

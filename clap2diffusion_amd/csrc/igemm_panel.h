@@ -243,7 +243,7 @@ __device__ __forceinline__ void panel_wait_vm() {
 // Bias and residual go through buffer loads (a missing bias reads zeros past num_records), so
 // their count in the vmcnt stream is a compile-time constant.
 template <int EPI>
-__global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int nsplit) {
+__global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int nsplit, int stagger) {
     constexpr int BM = kPanelRows, NKB = 5, BLK = BM * 128, A_BYTES = NKB * BLK, BSLOT = 32 * 128;
     constexpr int NST = EPI == PE_GEGLU ? 8 : 16;          // stores per block
     constexpr int NRES = EPI == PE_RESID ? 18 : 2;         // bias (2) + residual (16) loads per block
@@ -289,6 +289,11 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
     __syncthreads();
     C2D_PSTAMP(1);
     if (j0 >= nblk) return;   // wave-uniform; no barrier follows
+    // waves 4-7 (the second wave of each SIMD) start `stagger` x 2048 cycles late, so that on every
+    // SIMD one wave's epilogue (VALU, stores) runs beside its partner's K loop (MFMA) instead of
+    // every wave of the chip storing at once
+    if (wave >= 4)
+        for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(32);
     int sbi = 0;   // stamp block index (diagnostic builds)
     (void)sbi;
 
@@ -414,7 +419,7 @@ static void launch_panel_dma(IgemmParams& p, hipStream_t s) {
     ensure_lds<igemm_panel_dma_kernel<EPI>>(smem);
     const int ns = panel_nsplit(p.M, p.cout);
     const int grid = (p.M + kPanelRows - 1) / kPanelRows * ns;
-    hipLaunchKernelGGL((igemm_panel_dma_kernel<EPI>), dim3(grid), dim3(512), smem, s, p, ns);
+    hipLaunchKernelGGL((igemm_panel_dma_kernel<EPI>), dim3(grid), dim3(512), smem, s, p, ns, tuning().panel_stagger);
 }
 
 // K = 320 / 640 only (panel_eligible: also no GEGLU + residual); 32-bit offsets into A (dma_eligible)

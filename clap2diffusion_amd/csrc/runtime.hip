@@ -32,6 +32,7 @@ const Tuning& tuning() {
         t.tail_split = env_int("C2D_TAIL_SPLIT", 1);   // 0: no image split of a quantisation tail (A/B)
         t.gemm_sp = env_int("C2D_GEMM_SP", 0);         // 1: tiles 40 / 41 run their software-pipelined twins 60 / 61
         t.panel_regb = env_int("C2D_PANEL_REGB", 0);   // 1: the K = 320 panel GEMM loads its weights into registers (A/B)
+        t.panel_stagger = env_int("C2D_PANEL_STAGGER", 2);   // panel GEMM: late start of waves 4-7, x 2048 cycles
         t.attn_negc = env_int("C2D_ATTN_NEGC", 1);
         t.attn_res = env_int("C2D_ATTN_RES", 1);
         t.attn_w8 = env_int("C2D_ATTN_W8", 1);
