@@ -1,5 +1,8 @@
 """Summarise a rocprofv3 kernel_trace.csv: per (kernel, grid) totals and per family.
-usage: python scripts/kt_summary.py kernel_trace.csv [batches]"""
+usage: python scripts/kt_summary.py kernel_trace.csv [batches] [ledger.txt steps]
+With a step ledger (scripts/ledger.py) and the DDIM steps per batch, each MFMA family's trace time is
+set against the ledger's algorithmic FLOP: fraction of the 2.5 PF/s dense peak, time-weighted over
+the family's kernels in the trace (the igemm family = 3x3 + 1x1 + GEGLU + the split-K combine)."""
 import collections
 import csv
 import sys
@@ -54,5 +57,20 @@ print(f"device idle between kernels (gaps < 100 us): {gap / 1e3 / nb:.1f} ms per
 print(f"total {tot / 1e3:.1f} ms kernel time ({tot / 1e3 / nb:.1f} ms per batch over {nb:g} batches)")
 for f, v in sorted(fam.items(), key=lambda kv: -kv[1]):
     print(f"  {f:10s} {v / 1e3 / nb:8.1f} ms/batch {100 * v / tot:5.1f}%")
+if len(sys.argv) > 4:
+    led, steps = {}, float(sys.argv[4])
+    for line in open(sys.argv[3]):
+        f = line.split()
+        if len(f) == 9 and f[0] in ("igemm", "conv3x3", "gemm1x1", "geglu", "attention"):
+            led[f[0]] = float(f[4]) * 1e9   # GFLOP per step
+    tr = {"conv3x3": fam["conv3x3"], "gemm1x1+geglu": fam["gemm1x1"], "attention": fam["attention"],
+          "igemm": fam["conv3x3"] + fam["gemm1x1"] + fam["splitk"] + fam["gemm_reg"]}
+    fl = {"conv3x3": led.get("conv3x3", 0), "gemm1x1+geglu": led.get("gemm1x1", 0) + led.get("geglu", 0),
+          "attention": led.get("attention", 0), "igemm": led.get("igemm", 0)}
+    print(f"family MFMA fraction over the trace (ledger FLOP x {steps:g} steps per batch / trace time per batch):")
+    for f in ("igemm", "conv3x3", "gemm1x1+geglu", "attention"):
+        t = tr[f] / 1e6 / nb   # seconds per batch
+        if t > 0:
+            print(f"  {f:14s} {fl[f] * steps / 1e12:8.1f} TFLOP / {t * 1e3:7.1f} ms = {fl[f] * steps / t / 2.5e15:.3f}")
 for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])[:70]:
     print(f"{v[1] / 1e3:9.2f} ms {100 * v[1] / tot:5.1f}% {v[0]:6d} {v[1] / v[0]:9.1f}us grid={k[1]} {k[0]}")
