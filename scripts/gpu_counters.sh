@@ -14,8 +14,8 @@ for name in ${NAMES:-conv attn}; do
   case $name in
     conv[0-9]*) export C2D_GEMM_TILE=${name#conv}; PROG="python3 -u scripts/roof_kernel.py 5"; FILT=igemm ;;
     conv*) PROG="python3 -u scripts/roof_kernel.py 5"; FILT=igemm ;;
-    attn9216) PROG="python3 -u scripts/roof_attn.py 5 9216 8"; FILT=attn_fwd ;;
-    attn*) PROG="python3 -u scripts/roof_attn.py 5"; FILT=attn_fwd ;;
+    attn9216) PROG="python3 -u scripts/roof_attn.py 5 9216 8"; FILT=attn ;;
+    attn*) PROG="python3 -u scripts/roof_attn.py 5"; FILT=attn ;;
   esac
   i=0
   : > gpurun_out/pmc/${name}_counters.txt

@@ -16,6 +16,7 @@ The step itself is replayed as its captured graph and timed too: its time minus 
 rows is what the ledger does not attribute (torch copies, launch gaps, cross-op cache effects).
 
   python scripts/ledger.py --batch 8 [--res 64] [--reps 10] [--out profiles/r05_ledger_c3.txt]
+  python scripts/ledger.py --vae --batch 8 --res 64     (one VAE decode of 8 latents instead)
 bench.py imports `step_ledger` for roofline.family_frac.
 """
 from __future__ import annotations
@@ -157,14 +158,11 @@ def _time_graph(fn, reps: int, tries: int = 3) -> float:
     return best
 
 
-def step_ledger(den, reps: int = 10):
-    """Ledger of one step of a GraphDenoiser `den` (its eager body); -> (rows, families, meta).
-    rows: dicts sorted by lost us per step.  The denoiser's step counter is restored."""
-    idx0 = den.step_idx.clone()
-    den.step_idx.zero_()
+def call_ledger(run, reps: int = 10):
+    """Ledger of the c2d calls one invocation of run() issues; -> (rows, families, n_calls)."""
     rec = Recorder()
     with torch.no_grad(), rec:
-        den._body()
+        run()
     torch.cuda.synchronize()
     groups = collections.OrderedDict()
     for name, b, out in rec.calls:
@@ -195,15 +193,24 @@ def step_ledger(den, reps: int = 10):
         for f in (r["family"], "igemm" if r["op"] == "conv" else None, "all"):
             if f is None:
                 continue
-            s = fams.setdefault(f, dict(calls=0, us=0.0, flop=0.0, bytes=0.0, roof_us=0.0))
-            s["calls"] += r["calls"]
-            s["us"] += r["calls"] * r["us"]
-            s["flop"] += r["calls"] * r["flop"]
-            s["bytes"] += r["calls"] * r["bytes"]
-            s["roof_us"] += r["calls"] * r["roof_us"]
-    for s in fams.values():
-        s["frac"] = s["roof_us"] / s["us"] if s["us"] else 0.0
-        s["mfma_frac"] = s["flop"] / (s["us"] * 1e-6) / PEAK_FLOPS if s["us"] else 0.0
+            s_ = fams.setdefault(f, dict(calls=0, us=0.0, flop=0.0, bytes=0.0, roof_us=0.0))
+            s_["calls"] += r["calls"]
+            s_["us"] += r["calls"] * r["us"]
+            s_["flop"] += r["calls"] * r["flop"]
+            s_["bytes"] += r["calls"] * r["bytes"]
+            s_["roof_us"] += r["calls"] * r["roof_us"]
+    for s_ in fams.values():
+        s_["frac"] = s_["roof_us"] / s_["us"] if s_["us"] else 0.0
+        s_["mfma_frac"] = s_["flop"] / (s_["us"] * 1e-6) / PEAK_FLOPS if s_["us"] else 0.0
+    return rows, fams, len(rec.calls)
+
+
+def step_ledger(den, reps: int = 10):
+    """Ledger of one step of a GraphDenoiser `den` (its eager body); -> (rows, families, meta).
+    rows: dicts sorted by lost us per step.  The denoiser's step counter is restored."""
+    idx0 = den.step_idx.clone()
+    den.step_idx.zero_()
+    rows, fams, ncalls = call_ledger(den._body, reps)
     step_us = None
     if den.graph is not None:
         ts = []
@@ -217,16 +224,27 @@ def step_ledger(den, reps: int = 10):
             ts.append(e0.elapsed_time(e1) * 1e3)
         step_us = min(ts)
     den.step_idx.copy_(idx0)
-    meta = dict(n_calls=len(rec.calls), unique=len(rows), step_us=step_us, n=2 * den.b, res=den.h)
+    meta = dict(n_calls=ncalls, unique=len(rows), step_us=step_us, n=2 * den.b, res=den.h, what="denoise step")
+    return rows, fams, meta
+
+
+def vae_ledger(vae, latents, reps: int = 5):
+    """Ledger of one VAE decode of `latents` [B, 4, h, w]; the whole decode timed as a graph too."""
+    rows, fams, ncalls = call_ledger(lambda: vae(latents), reps)
+    whole = _time_graph(lambda: vae(latents), 1)
+    meta = dict(n_calls=ncalls, unique=len(rows), step_us=whole, n=latents.shape[0], res=latents.shape[-1],
+                what="VAE decode")
     return rows, fams, meta
 
 
 def format_ledger(rows, fams, meta) -> str:
     tot = fams["all"]["us"]
-    L = [f"# step ledger: N = {meta['n']} (CFG pair x {meta['n'] // 2}), {meta['res']}^2 latent; "
+    what = meta.get("what", "denoise step")
+    head = (f"N = {meta['n']} (CFG pair x {meta['n'] // 2})" if what == "denoise step" else f"B = {meta['n']}")
+    L = [f"# {what} ledger: {head}, {meta['res']}^2 latent; "
          f"{meta['n_calls']} recorded c2d calls, {meta['unique']} unique signatures",
-         f"# sum of rows {tot / 1e3:.3f} ms per step" + (
-             f"; captured step graph {meta['step_us'] / 1e3:.3f} ms (unattributed {(meta['step_us'] - tot) / 1e3:.3f} ms)"
+         f"# sum of rows {tot / 1e3:.3f} ms per {what}" + (
+             f"; captured graph {meta['step_us'] / 1e3:.3f} ms (unattributed {(meta['step_us'] - tot) / 1e3:.3f} ms)"
              if meta["step_us"] else ""),
          "# roofs: 2.5 PF/s dense fp16 MFMA, 8 TB/s HBM; frac = roof_us / us; lost = calls x (us - roof_us)",
          "",
@@ -250,7 +268,23 @@ def main():
     ap.add_argument("--res", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--vae", action="store_true", help="ledger of one VAE decode of B latents instead")
     a = ap.parse_args()
+    if a.vae:
+        from clap2diffusion_amd.vae import VAEDecoder
+        from clap2diffusion_amd.weights import synth_vae_decoder
+        dev = torch.device("cuda")
+        vae = VAEDecoder().to(dev)
+        vae.load_diffusers_state_dict(synth_vae_decoder(0))
+        lat = torch.randn(a.batch, 4, a.res, a.res, generator=torch.Generator().manual_seed(0)).to(dev)
+        with torch.no_grad():
+            vae(lat)
+        torch.cuda.synchronize()
+        txt = format_ledger(*vae_ledger(vae, lat, a.reps))
+        print(txt, flush=True)
+        if a.out:
+            Path(a.out).write_text(txt)
+        return
     from clap2diffusion_amd.processor import AudioProcessorManager
     from clap2diffusion_amd.sampler import GraphDenoiser
     from clap2diffusion_amd.scheduler import DDIMScheduler

@@ -739,6 +739,21 @@ def test_attention_wide_scores(dev, d):
     close(out, ref)
 
 
+@pytest.mark.parametrize("lq,lk,scale", [(300, 256, 1.0), (192, 320, 12.0), (520, 1024, 4.0)])
+def test_attention_d40_w8(dev, lq, lk, scale):
+    """The 8-wave d = 40 kernel (lk % 64 == 0, lk >= 256, no mask): a ragged last 256-query block,
+    and scores of std ~12 / ~4 so the first tile rebases the running max and later tiles rescale
+    (the lazy 2^8 test)."""
+    b, h, d = 2, 4, 40
+    q = gen(b * lq, h * d, seed=47) * scale
+    k = gen(b * lk, h * d, seed=48)
+    v = gen(b * lk, h * d, seed=49)
+    k[7] -= 3.0
+    ref = attn_ref(q, k, v, b, h, lq, lk, d)
+    out = ops.attention(q.half().to(dev), k.half().to(dev), v.half().to(dev), b, h, lq, lk, d)
+    close(out, ref)
+
+
 def test_groupnorm_large_mean(dev):
     n, c, hw = 2, 640, 1024
     x = gen(n, c, 32, 32, seed=43) + 30.0
