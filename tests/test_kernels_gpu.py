@@ -930,6 +930,29 @@ def test_groupnorm_two_launch_matches_three(dev, n, h, w, c0, c1, groups, silu):
     assert (pad[:, border] == 0).all()
 
 
+# GroupNorm with |mean| >> std (the shifted per-block moments keep the variance exact) on the
+# plain and the zero-bordered layout, concatenated inputs included; two back-to-back calls give
+# bit-identical outputs
+@pytest.mark.parametrize("n,h,c0,c1,mean", [(4, 64, 320, 0, 200.0), (16, 32, 640, 0, -50.0), (2, 64, 320, 320, 80.0)])
+def test_groupnorm_large_mean(dev, n, h, c0, c1, mean):
+    c = c0 + c1
+    x0 = gen(n, c0, h, h, seed=75) + mean
+    x1 = gen(n, c1, h, h, seed=76) * 2 + mean if c1 else None
+    gamma, beta = gen(c, seed=77) * 0.1 + 1, gen(c, seed=78) * 0.1
+    a = nhwc(x0).half().to(dev)
+    b = nhwc(x1).half().to(dev) if c1 else None
+    ref = F.silu(F.group_norm(torch.cat([nchw(a.float().cpu())] + ([nchw(b.float().cpu())] if c1 else []), 1),
+                              32, gamma, beta, 1e-5))
+    g, bt = gamma.float().to(dev), beta.float().to(dev)
+    out = ops.group_norm(a, 32, 1e-5, g, bt, True, x2=b)
+    out2 = ops.group_norm(a, 32, 1e-5, g, bt, True, x2=b)
+    close(nchw(out), ref, tol_max=5e-3, tol_l2=1e-3)
+    assert torch.equal(out, out2)
+    pad = ops.group_norm(a, 32, 1e-5, g, bt, True, x2=b, pad=True)
+    assert torch.equal(pad[:, 1:-1, 1:-1], out)
+    assert (pad[:, 0] == 0).all() and (pad[:, -1] == 0).all() and (pad[:, :, 0] == 0).all() and (pad[:, :, -1] == 0).all()
+
+
 # VAE widths: the planner's 256x128 (128 channels) and 256x256 (256 / 512 channels)
 # variants of the 32x32 tile; torch fp32 on the device is the reference
 @pytest.mark.parametrize("n,h,cin,cout", [
