@@ -11,6 +11,7 @@ from clap2diffusion_amd import ops  # noqa: E402
 dev = torch.device("cuda")
 SHAPES = [  # name, batch, heads, lq, lk, d
     ("L0 self 4096x4096 d40", 16, 8, 4096, 4096, 40),
+    ("c5 L0 self 9216x9216 d40", 8, 8, 9216, 9216, 40),   # 768^2, B = 4 with CFG
     ("L0 cross 4096x77 d40", 16, 8, 4096, 77, 40),
     ("L1 self 1024x1024 d80", 16, 8, 1024, 1024, 80),
     ("L2 self 256x256 d160", 16, 8, 256, 256, 160),
