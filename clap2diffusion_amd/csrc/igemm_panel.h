@@ -44,10 +44,9 @@ __device__ __forceinline__ void panel_resid(const IgemmParams& p, f16x4 (&rv)[8]
     }
 }
 
-// Epilogue of one 128 x 32 block (acc[a][b]: column tile a, row tile b; lane holds row
-// m0 + 16 b + (lane & 15), columns 4 (lane >> 4) .. +3 of the tile): bias, residual or GEGLU,
-// fp16 stores of 8 B
-// bias of one block's two column tiles (prefetched with the residual)
+// bias of one block's two column tiles: the accumulators of the block start from it (loaded
+// during the previous block), so the epilogue adds no bias
+
 __device__ __forceinline__ void panel_bias(const IgemmParams& p, float4 (&bv)[2], int ncol0, int lane) {
     const int jb = ncol0 + 4 * (lane >> 4);
 #pragma unroll
@@ -55,9 +54,12 @@ __device__ __forceinline__ void panel_bias(const IgemmParams& p, float4 (&bv)[2]
         bv[a] = p.bias ? *reinterpret_cast<const float4*>(p.bias + jb + 16 * a) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// Epilogue of one 128 x 32 block (acc[a][b]: column tile a, row tile b; lane holds row
+// m0 + 16 b + (lane & 15), columns 4 (lane >> 4) .. +3 of the tile; bias already in acc):
+// residual or GEGLU, fp16 stores of 8 B
 template <int EPI>
 __device__ __forceinline__ void panel_epilogue(const IgemmParams& p, const f32x4 (&acc)[2][8], const f16x4 (&rv)[8][2],
-                                               const float4 (&bv)[2], int m0, int ncol0, int lane) {
+                                               int m0, int ncol0, int lane) {
     const int lr = lane & 15, lc = 4 * (lane >> 4);
     const int jo = EPI == PE_GEGLU ? (ncol0 >> 1) + lc : ncol0 + lc;   // output column of tile 0
     // stores through a buffer descriptor over the output: a row past M gets an offset past
@@ -69,19 +71,17 @@ __device__ __forceinline__ void panel_epilogue(const IgemmParams& p, const f32x4
         const int m = m0 + b * 16 + lr;
         const unsigned off = m < p.M ? (unsigned)(2 * (m * p.out_ld + jo)) : kOOB;
         if constexpr (EPI == PE_GEGLU) {
-            const float hb[4] = {bv[0].x, bv[0].y, bv[0].z, bv[0].w}, gb[4] = {bv[1].x, bv[1].y, bv[1].z, bv[1].w};
             f16x4 o;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (f16)((acc[0][b][r] + hb[r]) * gelu_sig(acc[1][b][r] + gb[r]));
+            for (int r = 0; r < 4; ++r) o[r] = (f16)(acc[0][b][r] * gelu_sig(acc[1][b][r]));
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ro, off, 0, 0);
         } else {
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
-                const float bb[4] = {bv[a].x, bv[a].y, bv[a].z, bv[a].w};
                 f16x4 o;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float v = acc[a][b][r] + bb[r];
+                    float v = acc[a][b][r];
                     if constexpr (EPI == PE_RESID) v += (float)rv[b][a][r];
                     o[r] = (f16)v;
                 }
@@ -137,6 +137,8 @@ __global__ void __launch_bounds__(512) igemm_panel_kernel(IgemmParams p, int nsp
         bq[s][0] = *reinterpret_cast<const f16x8*>(pb0 + boff(s));
         bq[s][1] = *reinterpret_cast<const f16x8*>(pb1 + boff(s));
     }
+    float4 bv[2];   // bias of the next column block: its accumulators start from it
+    panel_bias(p, bv, 32 * jfirst, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (j0 >= nblk) return;   // wave-uniform; no barrier follows
@@ -167,13 +169,12 @@ __global__ void __launch_bounds__(512) igemm_panel_kernel(IgemmParams p, int nsp
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4){bv[a].x, bv[a].y, bv[a].z, bv[a].w};
         f16x4 rv[8][2];
-        float4 bv[2];
 #pragma unroll
         for (int ks = 0; ks < NK32; ++ks) {
-            if (ks == NK32 - PD) {   // epilogue operands, ahead of the next block's first weight loads
-                panel_bias(p, bv, 32 * j, lane);
+            if (ks == NK32 - PD) {   // epilogue operands and the next block's bias, ahead of its first weights
+                panel_bias(p, bv, 32 * jn, lane);
                 if constexpr (EPI == PE_RESID) panel_resid(p, rv, m0, 32 * j, lane);
             }
             aread(ks + 1 < NK32 ? ks + 1 : 0, fa[(ks + 1) & 1]);
@@ -203,7 +204,7 @@ __global__ void __launch_bounds__(512) igemm_panel_kernel(IgemmParams p, int nsp
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        panel_epilogue<EPI>(p, acc, rv, bv, m0, 32 * j, lane);
+        panel_epilogue<EPI>(p, acc, rv, m0, 32 * j, lane);
         pb0 = pn0;
         pb1 = pn1;
     };
@@ -285,6 +286,15 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
     };
     const int jfirst = j0 < nblk ? j0 : 0;
     bdma(jfirst, 0, 0);
+    const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias ? (unsigned)(p.cout * 4) : 0u);
+    float4 bv[2];   // bias of the next column block: its accumulators start from it
+    auto bload = [&](int j) __attribute__((always_inline)) {
+        const int lc = 32 * j + 4 * (lane >> 4);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+            bv[a] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rbias, 4 * (lc + 16 * a), 0, 0));
+    };
+    bload(jfirst);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     C2D_PSTAMP(1);
@@ -304,7 +314,6 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
 #pragma unroll
         for (int a = 0; a < 2; ++a) fbo[a][h] = lds_off(16 * a + (lane & 15), h * 4 + (lane >> 4));
     }
-    const __amdgpu_buffer_rsrc_t rbias = make_rsrc(p.bias, p.bias ? (unsigned)(p.cout * 4) : 0u);
     const __amdgpu_buffer_rsrc_t rres = make_rsrc(p.resid, p.resid ? (unsigned)((size_t)p.M * p.resid_ld * 2) : 0u);
     f16x8 fa[2][8];
     auto aread = [&](int ks, f16x8 (&dst)[8]) {
@@ -321,16 +330,13 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            for (int b = 0; b < 8; ++b) acc[a][b] = (f32x4){bv[a].x, bv[a].y, bv[a].z, bv[a].w};
         f16x4 rv[8][2];
-        float4 bv[2];
 #pragma unroll
         for (int t = 0; t < NKB; ++t) {
-            if (t == NKB - 1) {   // epilogue operands, ahead of the next block's first weights
+            if (t == NKB - 1) {   // epilogue operands and the next block's bias, ahead of its first weights
                 const int lc = 32 * j + 4 * (lane >> 4);
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-                    bv[a] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rbias, 4 * (lc + 16 * a), 0, 0));
+                bload(jn);
                 if constexpr (EPI == PE_RESID) {
 #pragma unroll
                     for (int b = 0; b < 8; ++b) {
@@ -368,7 +374,7 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
             }
         }
         C2D_PSTAMP(8 + 8 * sbi);
-        panel_epilogue<EPI>(p, acc, rv, bv, m0, 32 * j, lane);
+        panel_epilogue<EPI>(p, acc, rv, m0, 32 * j, lane);
         C2D_PSTAMP(9 + 8 * sbi);
         ++sbi;
         par ^= 1;
