@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be loaded first: the library binds to torch's 
 
 LIB_PATH = Path(os.environ.get("C2D_LIB") or Path(__file__).resolve().parent / "libc2d_hip.so")  # C2D_LIB: A/B builds
 
-C2D_PRO_NONE, C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_SILU = 0, 1, 2, 3
+C2D_PRO_NONE, C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_SILU, C2D_PRO_LNFOLD = 0, 1, 2, 3, 4
 C2D_ACT = {None: 0, "none": 0, "geglu": 1, "gelu": 2, "relu": 3, "silu": 4, "quick_gelu": 5}
 ERRORS = {-1: "C2D_E_ARG", -2: "C2D_E_SHAPE", -3: "C2D_E_ALIGN", -4: "C2D_E_HIP"}
 
@@ -38,7 +38,7 @@ class ConvDesc(ctypes.Structure):
         ("gamma", c_void_p), ("beta", c_void_p), ("bias", c_void_p), ("act", c_int),
         ("temb", c_void_p), ("temb_ld", c_int), ("resid", c_void_p), ("resid_ld", c_int),
         ("out", c_void_p), ("out_ld", c_int), ("ws", c_void_p), ("ws_bytes", c_size_t),
-        ("src_pad", c_int),
+        ("src_pad", c_int), ("pro_eps", c_float),
     ]
 
 

@@ -56,6 +56,7 @@ struct IgemmParams {
     int abl;     // timing ablation bits (C2D_GEMM_ABL; 0 in production)
     int lds_epi; // 32x32 kernels: 1 = LDS-staged epilogue (C2D_GEMM_LDSEPI or alignment), 0 = direct
     int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_GEMM_KORDER, default 1)
+    float pro_eps;   // C2D_PRO_LNFOLD: LayerNorm eps
 };
 
 // one accumulator quad of K slice `slice` into the split-K workspace, fp32 or rounded to fp16
@@ -1136,7 +1137,7 @@ static bool dma_eligible(const c2d_conv_desc* d) {
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);
     const int pd = d->src_pad ? 2 : 0;
     const size_t src_bytes = (size_t)d->n * (d->h + pd) * (d->w + pd) * (size_t)(d->c0 > d->c1 ? d->c0 : d->c1) * 2;
-    return (d->pro == C2D_PRO_NONE) && amode != AM_3X3_GEN && !d->up && gemm_mode() != 2 &&
+    return (d->pro == C2D_PRO_NONE || d->pro == C2D_PRO_LNFOLD) && amode != AM_3X3_GEN && !d->up && gemm_mode() != 2 &&
            (d->c1 == 0 || (d->c0 & 63) == 0) && src_bytes < (1u << 31) &&
            (size_t)d->cout * d->kpad * 2 < (1u << 31);  // 32-bit buffer offsets
 }
@@ -1146,7 +1147,8 @@ static bool dma_eligible(const c2d_conv_desc* d) {
 // epilogue's alignment
 static bool panel_eligible(const c2d_conv_desc* d) {
     return d->ksize == 1 && d->c1 == 0 && (d->c0 == 320 || d->c0 == 640) && d->kpad == d->c0 && (d->cout & 31) == 0 &&
-           d->pro == C2D_PRO_NONE && !d->temb && (d->act == C2D_ACT_NONE || (d->act == C2D_ACT_GEGLU && !d->resid)) &&
+           (d->pro == C2D_PRO_NONE || (d->pro == C2D_PRO_LNFOLD && !d->resid)) &&
+           !d->temb && (d->act == C2D_ACT_NONE || (d->act == C2D_ACT_GEGLU && !d->resid)) &&
            epi_direct_ok(d) && dma_eligible(d) && (size_t)d->n * d->oh * d->ow * d->out_ld * 2 < (1u << 31);
 }
 
@@ -1204,6 +1206,7 @@ static size_t tail_ws_bytes(const c2d_conv_desc* d, int n1) {
 extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     if (!d || d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return 0;
     if (!dma_eligible(d)) return 0;
+    if (d->pro == C2D_PRO_LNFOLD) return 0;   // the panel GEMM, one slice
     const long M = (long)d->n * d->oh * d->ow;
     const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
     if (const int n1 = tail_images(d, pl)) return tail_ws_bytes(d, n1);
@@ -1215,6 +1218,12 @@ extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* 
     if (d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return C2D_E_SHAPE;
     if (!dma_eligible(d)) {
         *tile_id = 0;
+        *ksplit = 1;
+        return C2D_OK;
+    }
+    if (d->pro == C2D_PRO_LNFOLD) {   // the panel GEMM or nothing
+        if (!panel_eligible(d)) return C2D_E_SHAPE;
+        *tile_id = 70;
         *ksplit = 1;
         return C2D_OK;
     }
@@ -1270,7 +1279,9 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     if (d->bias && ((uintptr_t)d->bias & 15)) return C2D_E_ALIGN;
     if (d->pro == C2D_PRO_GN && (!d->pro_a || !d->pro_b || (cin & 3))) return C2D_E_ARG;
     if (d->pro == C2D_PRO_LN && (!d->pro_a || !d->gamma || !d->beta)) return C2D_E_ARG;
-    if (d->pro < 0 || d->pro > 3 || d->act < 0 || d->act > 5) return C2D_E_ARG;
+    if (d->pro < 0 || d->pro > 4 || d->act < 0 || d->act > 5) return C2D_E_ARG;
+    if (d->pro == C2D_PRO_LNFOLD && !(d->pro_eps > 0.f)) return C2D_E_ARG;
+    if (d->pro == C2D_PRO_LNFOLD && !panel_eligible(d)) return C2D_E_SHAPE;   // only the panel GEMM folds LN
     if (d->stride != 1 && d->stride != 2) return C2D_E_SHAPE;
     if (d->ksize == 1 && (d->stride != 1 || d->up || d->oh != d->h || d->ow != d->w)) return C2D_E_SHAPE;
     if (d->up && d->stride != 1) return C2D_E_SHAPE;
@@ -1296,6 +1307,7 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     p.pro = d->pro; p.pro_silu = d->pro_silu;
     p.pro_a = d->pro_a; p.pro_b = d->pro_b; p.gamma = d->gamma; p.beta = d->beta;
     p.bias = d->bias; p.act = d->act;
+    p.pro_eps = d->pro_eps;
     p.temb = (const f16*)d->temb; p.temb_ld = d->temb_ld;
     p.resid = (const f16*)d->resid; p.resid_ld = d->resid_ld;
     p.out = (f16*)d->out; p.out_ld = d->out_ld;
@@ -1314,6 +1326,7 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     const long t128 = (long)((p.M + 127) / 128) * ((d->cout + 127) / 128);
     if (dma) {
         DmaPlan pl = fixed ? *fixed : plan_for(p.M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
+        if (d->pro == C2D_PRO_LNFOLD) pl = {70, 1, d->kpad / 64};   // validated above: panel_eligible
         if (pl.split > 1) {
             const size_t need = (size_t)pl.split * p.M * d->cout * sizeof(float);
             if (d->ws && d->ws_bytes >= need && aligned16(d->ws)) {

@@ -91,7 +91,56 @@ __device__ __forceinline__ void panel_epilogue(const IgemmParams& p, const f32x4
     }
 }
 
-template <int NK32, int PD, int EPI>
+// LayerNorm in place on a landed panel (C2D_PRO_LNFOLD): row r of the 128 is normalised,
+// (x - mean) * rstd rounded to fp16 as the LayerNorm kernel's output is, by the four lanes
+// 4 (r % 16) .. +3 of wave r / 16: each holds NKB * 2 of the row's NKB * 8 16-B chunks (the
+// swizzled image's slots, any order) in registers through both passes (fixed order), the quarters
+// combining by two lane exchanges.  Rows past M were DMA'd as zeros and stay zero.  The caller
+// synchronises the workgroup before the panel is read.
+template <int NKB>
+__device__ __forceinline__ void panel_ln_inplace(char* smem, int wave, int lane, float eps) {
+    constexpr int BLK = kPanelRows * 128, NC = NKB * 2;
+    constexpr float inv_k = 1.0f / (NKB * 64);
+    const int row = wave * 16 + (lane >> 2), qd = lane & 3;
+    char* rb = smem + (row >> 3) * 1024 + (row & 7) * 128;
+    f16x8 v[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        const int c = qd * NC + i;
+        v[i] = *reinterpret_cast<const f16x8*>(rb + (c >> 3) * BLK + (c & 7) * 16);
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sm += (float)v[i][e];
+    sm += __shfl_xor(sm, 1);
+    sm += __shfl_xor(sm, 2);
+    const float mean = sm * inv_k;
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float d = (float)v[i][e] - mean;
+            sq = fmaf(d, d, sq);
+        }
+    sq += __shfl_xor(sq, 1);
+    sq += __shfl_xor(sq, 2);
+    const float rstd = 1.0f / sqrtf(sq * inv_k + eps);
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+        f16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (f16)(((float)v[i][e] - mean) * rstd);
+        const int c = qd * NC + i;
+        *reinterpret_cast<f16x8*>(rb + (c >> 3) * BLK + (c & 7) * 16) = o;
+    }
+}
+
+// LNF (C2D_PRO_LNFOLD): a LayerNorm folded in -- once the panel has landed it is normalised in
+// place (panel_ln_inplace); the GEMM then runs on W diag(gamma) with bias b + W beta
+template <int NK32, int PD, int EPI, bool LNF = false>
 __global__ void __launch_bounds__(512) igemm_panel_kernel(IgemmParams p, int nsplit) {
     static_assert(NK32 % PD == 0 && (PD & 1) && !(NK32 & 1), "the register ring restarts with every column block; line pairs");
     constexpr int BM = kPanelRows, NKB = NK32 / 2, BLK = BM * 128;   // bytes per 64-channel block
@@ -141,6 +190,10 @@ __global__ void __launch_bounds__(512) igemm_panel_kernel(IgemmParams p, int nsp
     panel_bias(p, bv, 32 * jfirst, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if constexpr (LNF) {
+        panel_ln_inplace<NKB>(smem, wave, lane, p.pro_eps);
+        __syncthreads();
+    }
     if (j0 >= nblk) return;   // wave-uniform; no barrier follows
 
     int fa0[2];
@@ -243,7 +296,8 @@ __device__ __forceinline__ void panel_wait_vm() {
 // measured 20 % slower over the whole kernel than whole-line loads (profiles/r05_panel_gemm.txt).
 // Bias and residual go through buffer loads (a missing bias reads zeros past num_records), so
 // their count in the vmcnt stream is a compile-time constant.
-template <int EPI>
+// LNF (C2D_PRO_LNFOLD): as igemm_panel_kernel's
+template <int EPI, bool LNF = false>
 __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int nsplit, int stagger) {
     constexpr int BM = kPanelRows, NKB = 5, BLK = BM * 128, A_BYTES = NKB * BLK, BSLOT = 32 * 128;
     constexpr int NST = EPI == PE_GEGLU ? 8 : 16;          // stores per block
@@ -298,6 +352,10 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     C2D_PSTAMP(1);
+    if constexpr (LNF) {
+        panel_ln_inplace<NKB>(smem, wave, lane, p.pro_eps);
+        __syncthreads();
+    }
     if (j0 >= nblk) return;   // wave-uniform; no barrier follows
     // waves 4-7 (the second wave of each SIMD) start `stagger` x 2048 cycles late, so that on every
     // SIMD one wave's epilogue (VALU, stores) runs beside its partner's K loop (MFMA) instead of
@@ -392,14 +450,14 @@ static int panel_nsplit(int M, int cout) {
     return ns < 1 ? 1 : (ns > maxs ? maxs : ns);
 }
 
-template <int NK32, int EPI>
+template <int NK32, int EPI, bool LNF = false>
 static void launch_panel(IgemmParams& p, hipStream_t s) {
     constexpr int smem = NK32 / 2 * kPanelRows * 128;
     static_assert(smem <= 160 * 1024, "A panel too large");
-    ensure_lds<igemm_panel_kernel<NK32, 5, EPI>>(smem);
+    ensure_lds<igemm_panel_kernel<NK32, 5, EPI, LNF>>(smem);
     const int ns = panel_nsplit(p.M, p.cout);
     const int grid = (p.M + kPanelRows - 1) / kPanelRows * ns;
-    hipLaunchKernelGGL((igemm_panel_kernel<NK32, 5, EPI>), dim3(grid), dim3(512), smem, s, p, ns);
+    hipLaunchKernelGGL((igemm_panel_kernel<NK32, 5, EPI, LNF>), dim3(grid), dim3(512), smem, s, p, ns);
 }
 
 template <int NK32>
@@ -419,18 +477,28 @@ extern "C" int c2d_debug_panel_stamps(unsigned long long* host, int n) {
 namespace c2d {
 #endif
 
-template <int EPI>
+template <int EPI, bool LNF = false>
 static void launch_panel_dma(IgemmParams& p, hipStream_t s) {
     constexpr int smem = 5 * kPanelRows * 128 + 8 * 2 * 32 * 128;   // 80 + 64 KiB
-    ensure_lds<igemm_panel_dma_kernel<EPI>>(smem);
+    ensure_lds<igemm_panel_dma_kernel<EPI, LNF>>(smem);
     const int ns = panel_nsplit(p.M, p.cout);
     const int grid = (p.M + kPanelRows - 1) / kPanelRows * ns;
-    hipLaunchKernelGGL((igemm_panel_dma_kernel<EPI>), dim3(grid), dim3(512), smem, s, p, ns, tuning().panel_stagger);
+    hipLaunchKernelGGL((igemm_panel_dma_kernel<EPI, LNF>), dim3(grid), dim3(512), smem, s, p, ns,
+                       tuning().panel_stagger);
 }
 
-// K = 320 / 640 only (panel_eligible: also no GEGLU + residual); 32-bit offsets into A (dma_eligible)
+// K = 320 / 640 only (panel_eligible: also no GEGLU + residual); 32-bit offsets into A (dma_eligible).
+// A folded LayerNorm (C2D_PRO_LNFOLD) takes the LDS-DMA form at K = 320.
 static void run_panel(IgemmParams& p, hipStream_t s) {
-    if (p.kpad == 320 && !tuning().panel_regb) {
+    if (p.pro == C2D_PRO_LNFOLD) {
+        if (p.kpad == 320) {
+            if (p.act == C2D_ACT_GEGLU) launch_panel_dma<PE_GEGLU, true>(p, s);
+            else launch_panel_dma<PE_PLAIN, true>(p, s);
+        } else {
+            if (p.act == C2D_ACT_GEGLU) launch_panel<20, PE_GEGLU, true>(p, s);
+            else launch_panel<20, PE_PLAIN, true>(p, s);
+        }
+    } else if (p.kpad == 320 && !tuning().panel_regb) {
         if (p.act == C2D_ACT_GEGLU) launch_panel_dma<PE_GEGLU>(p, s);
         else if (p.resid) launch_panel_dma<PE_RESID>(p, s);
         else launch_panel_dma<PE_PLAIN>(p, s);

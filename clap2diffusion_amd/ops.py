@@ -84,12 +84,15 @@ def geglu_interleave(w: torch.Tensor, b: torch.Tensor | None):
 def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: int, bias=None, stride: int = 1,
          up: bool = False, x2: torch.Tensor | None = None, gn=None, gn_silu: bool = False, ln=None,
          silu_in: bool = False, act: str | None = None, temb: torch.Tensor | None = None,
-         resid: torch.Tensor | None = None, out: torch.Tensor | None = None, padded: bool = False) -> torch.Tensor:
+         resid: torch.Tensor | None = None, out: torch.Tensor | None = None, padded: bool = False,
+         ln_fold=None) -> torch.Tensor:
     """Implicit-GEMM conv / linear (c2d::conv2d_igemm).
 
     x: NHWC [N, H, W, C0] fp16 (or 2-D [M, C0] for a linear layer); padded: x is the
     zero-bordered [N, H + 2, W + 2, C0] of group_norm(pad=True) (3x3, stride 1, one source).
     gn: (scale, shift) fp32 [N, C0+C1]; ln: (stats [M, 2], gamma, beta).
+    ln_fold: eps of a LayerNorm folded into this linear: x is the LayerNorm's raw input
+    (weight = W diag(gamma), bias = b + W beta; fold_layernorm builds them), panel GEMM shapes only.
     """
     _require(x, "x")
     if x.dim() == 2:
@@ -119,8 +122,37 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
     gs, gh = gn if gn is not None else (None, None)
     ls, lg, lb = ln if ln is not None else (None, None, None)
     C2D.conv2d_igemm(x, weight, kpad, cout, ksize, stride, up, x2, gs, gh, gn_silu, ls, lg, lb, silu_in, bias,
-                     C2D_ACT[act], temb, resid, out, bool(padded))
+                     C2D_ACT[act], temb, resid, out, bool(padded), float(ln_fold or 0.0))
     return out
+
+
+@torch.no_grad()
+def fold_layernorm(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch.Tensor, beta: torch.Tensor,
+                   in_features: int):
+    """LayerNorm(gamma, beta) -> Linear(packed fp16 weight [cout][kpad], bias) as one GEMM over the
+    normalised rows (C2D_PRO_LNFOLD): (W diag(gamma) fp16, b + W beta fp32)."""
+    w = weight[:, :in_features].float()
+    wp = torch.zeros_like(weight)
+    wp[:, :in_features] = (w * gamma.float().view(1, -1)).to(F16)
+    b = w @ beta.float()
+    if bias is not None:
+        b = b + bias.float()
+    return wp.contiguous(), b.contiguous()
+
+
+@functools.lru_cache(maxsize=None)
+def panel_gemm(m: int, k: int, cout: int, geglu: bool) -> bool:
+    """Does c2d's planner run this 1x1 GEMM (m x k -> cout) on the panel GEMM (tile 70)?  Where it
+    does, a LayerNorm before it folds in (C2D_PRO_LNFOLD)."""
+    import ctypes
+    from ._lib import ConvDesc, check, lib
+    d = ConvDesc()
+    d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = k, 1, 1, m, 1, m, 1, 1
+    d.cout, d.kpad, d.act = cout, kpad_of(k), C2D_ACT["geglu" if geglu else None]
+    d.out_ld = cout // 2 if geglu else cout
+    tid, ks = ctypes.c_int(), ctypes.c_int()
+    check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
+    return tid.value == 70
 
 
 @functools.lru_cache(maxsize=None)

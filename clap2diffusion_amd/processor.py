@@ -92,14 +92,18 @@ class AttnProcessor(nn.Module):
     fuses_residual = True
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
-                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
+                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, _qkv: Optional[torch.Tensor] = None,
+                 **cross_attention_kwargs):
+        """_qkv: the self-attention's [B*L, 3*inner] projections already computed by the caller
+        (BasicTransformerBlock: norm1 folded into the QKV GEMM); hidden_states then only gives
+        the shape."""
         x, restore = _as_tokens(hidden_states)
         b, l, c = x.shape
         x2 = x.view(b * l, c)
         heads, d = attn.heads, attn.dim_head
         inner = heads * d
         if encoder_hidden_states is None:
-            qkv = ops.conv(x2, attn.w_qkv, attn.kpad_q, 3 * inner, ksize=1)
+            qkv = _qkv if _qkv is not None else ops.conv(x2, attn.w_qkv, attn.kpad_q, 3 * inner, ksize=1)
             if scale != 1.0:
                 qkv[:, :inner].mul_(scale)
             o = ops.attention(qkv[:, :inner], qkv[:, inner:2 * inner], qkv[:, 2 * inner:], b, heads, l, l, d,

@@ -18,13 +18,13 @@ import torch
 from torch import Tensor
 from torch.library import custom_op
 
-from ._lib import C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_NONE, C2D_PRO_SILU, ConvDesc, check, lib, ptr, stream_ptr
+from ._lib import C2D_PRO_GN, C2D_PRO_LN, C2D_PRO_LNFOLD, C2D_PRO_NONE, C2D_PRO_SILU, ConvDesc, check, lib, ptr, stream_ptr
 
 _CU = "cuda"
 
 
 def _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma,
-               ln_beta, silu_in, bias, act, temb, resid, out, src_pad=False) -> ConvDesc:
+               ln_beta, silu_in, bias, act, temb, resid, out, src_pad=False, lnf_eps=0.0) -> ConvDesc:
     if x.dim() == 2:
         n, h, w = 1, 1, x.shape[0]
         c0 = x.shape[1]
@@ -43,7 +43,9 @@ def _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift,
     d.n, d.h, d.w, d.oh, d.ow = n, h, w, oh, ow
     d.ksize, d.stride, d.up = ksize, stride, int(up)
     d.weight = ptr(weight); d.cout = cout; d.kpad = kpad
-    if gn_scale is not None:
+    if lnf_eps > 0.0:   # LayerNorm folded into the panel GEMM (weight = W diag(gamma), bias = b + W beta)
+        d.pro = C2D_PRO_LNFOLD; d.pro_eps = lnf_eps
+    elif gn_scale is not None:
         d.pro = C2D_PRO_GN; d.pro_silu = int(gn_silu); d.pro_a = ptr(gn_scale); d.pro_b = ptr(gn_shift)
     elif ln_stats is not None:
         d.pro = C2D_PRO_LN; d.pro_a = ptr(ln_stats); d.gamma = ptr(ln_gamma); d.beta = ptr(ln_beta)
@@ -71,11 +73,12 @@ def conv2d_igemm(x: Tensor, weight: Tensor, kpad: int, cout: int, ksize: int, st
                  x2: Optional[Tensor], gn_scale: Optional[Tensor], gn_shift: Optional[Tensor], gn_silu: bool,
                  ln_stats: Optional[Tensor], ln_gamma: Optional[Tensor], ln_beta: Optional[Tensor], silu_in: bool,
                  bias: Optional[Tensor], act: int, temb: Optional[Tensor], resid: Optional[Tensor],
-                 out: Tensor, src_pad: bool = False) -> None:
+                 out: Tensor, src_pad: bool = False, lnf_eps: float = 0.0) -> None:
     """c2d_conv2d_igemm (+ its split-K workspace, sized by c2d_conv2d_igemm_workspace_size).
-    src_pad: x is the zero-bordered layout [n][h + 2][w + 2][c] (c2d_groupnorm_pad)."""
+    src_pad: x is the zero-bordered layout [n][h + 2][w + 2][c] (c2d_groupnorm_pad).
+    lnf_eps > 0: a LayerNorm (that eps) folded into the GEMM (C2D_PRO_LNFOLD)."""
     d = _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma,
-                   ln_beta, silu_in, bias, act, temb, resid, out, src_pad)
+                   ln_beta, silu_in, bias, act, temb, resid, out, src_pad, lnf_eps)
     wsb = lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
     if wsb:
         ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
@@ -89,7 +92,7 @@ def conv2d_igemm(x: Tensor, weight: Tensor, kpad: int, cout: int, ksize: int, st
 
 @conv2d_igemm.register_fake
 def _(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma, ln_beta,
-      silu_in, bias, act, temb, resid, out, src_pad=False):
+      silu_in, bias, act, temb, resid, out, src_pad=False, lnf_eps=0.0):
     return None
 
 

@@ -48,6 +48,9 @@ from .weights import SD15_UNET
 
 # ff.net.2 folded into proj_out (Transformer2DModel): read once at import, A/B switch only
 FOLD_FF_OUT = os.environ.get("C2D_FOLD_FF_OUT", "1") != "0"
+# norm1 / norm3 folded into the QKV / GEGLU GEMMs where those run on the panel GEMM (K = 320):
+# A/B switch only (C2D_LN_FOLD=0 materialises the LayerNorm outputs)
+FOLD_LN = os.environ.get("C2D_LN_FOLD", "1") != "0"
 
 
 class Attention(nn.Module):
@@ -142,6 +145,31 @@ class BasicTransformerBlock(nn.Module):
         self.attn2 = Attention(dim, cross_dim, heads)
         self.norm3 = HLayerNorm(dim)
         self.ff = FeedForward(dim)
+        # LayerNorm folded into the GEMM after it (C2D_PRO_LNFOLD, the panel GEMM's K = 320 / 640: the
+        # kernel normalises its LDS panel in place): W diag(gamma) and b + W beta for norm1 -> fused
+        # QKV and norm3 -> GEGLU (finalize); used where the planner runs those GEMMs on the panel kernel
+        self.lnf = dim in (320, 640)
+        inner = self.attn1.heads * self.attn1.dim_head
+        kp = self.attn1.kpad_q
+        for name, rows in (("qkv", 3 * inner), ("ff", self.ff.net[0].proj.out_features)):
+            self.register_buffer(f"lnf_{name}_w", torch.zeros(rows, kp, dtype=torch.float16) if self.lnf else None,
+                                 persistent=False)
+            self.register_buffer(f"lnf_{name}_b", torch.zeros(rows) if self.lnf else None, persistent=False)
+
+    @torch.no_grad()
+    def finalize(self) -> None:
+        if not self.lnf:
+            return
+        c = self.norm1.c
+        wq = torch.cat([self.attn1.to_q.weight, self.attn1.to_k.weight, self.attn1.to_v.weight], 0)
+        for name, w, b, norm in (("qkv", wq, None, self.norm1),
+                                 ("ff", self.ff.net[0].proj.weight, self.ff.net[0].proj.bias, self.norm3)):
+            wf, bf = ops.fold_layernorm(w, b, norm.weight, norm.bias, c)
+            getattr(self, f"lnf_{name}_w").copy_(wf)
+            getattr(self, f"lnf_{name}_b").copy_(bf)
+
+    def _lnf_on(self, m: int, cout: int, geglu: bool) -> bool:
+        return FOLD_LN and self.lnf and ops.panel_gemm(m, self.norm1.c, cout, geglu)
 
     def _attend(self, attn: Attention, x, h, ehs, mask, kwargs):
         if getattr(attn.processor, "fuses_residual", False):
@@ -163,8 +191,13 @@ class BasicTransformerBlock(nn.Module):
         return h
 
     def ff_inner(self, h2: torch.Tensor) -> torch.Tensor:
-        """GEGLU(LN3(h)) [M, 4C]: the feed-forward up to its output Linear."""
-        return self.ff.net[0].proj(self.norm3(h2), act="geglu")
+        """GEGLU(LN3(h)) [M, 4C]: the feed-forward up to its output Linear (LN3 folded into the
+        GEMM on panel-GEMM shapes)."""
+        proj = self.ff.net[0].proj
+        if self._lnf_on(h2.shape[0], proj.out_features, True):
+            return ops.conv(h2, self.lnf_ff_w, proj.kpad, proj.out_features, ksize=1, bias=self.lnf_ff_b,
+                            act="geglu", ln_fold=self.norm3.eps)
+        return proj(self.norm3(h2), act="geglu")
 
     def forward_attn(self, h: torch.Tensor, ehs: torch.Tensor, cross_attention_kwargs: dict,
                      encoder_attention_mask: torch.Tensor | None = None,
@@ -176,7 +209,15 @@ class BasicTransformerBlock(nn.Module):
         is copied into the second half before attn2, the first op where the [uncond, cond] halves
         differ (UNet2DConditionModel.forward_nhwc)."""
         kw = cross_attention_kwargs or {}
-        h = self._attend(self.attn1, self.norm1(h), h, None, None, kw)
+        b, l, c = h.shape
+        inner = self.attn1.heads * self.attn1.dim_head
+        if type(self.attn1.processor) is AttnProcessor and self._lnf_on(b * l, 3 * inner, False):
+            # norm1 folded into the fused QKV GEMM; the stock processor takes the projections
+            qkv = ops.conv(h.view(b * l, c), self.lnf_qkv_w, self.attn1.kpad_q, 3 * inner, ksize=1,
+                           bias=self.lnf_qkv_b, ln_fold=self.norm1.eps)
+            h = self._attend(self.attn1, h, h, None, None, dict(kw, _qkv=qkv))
+        else:
+            h = self._attend(self.attn1, self.norm1(h), h, None, None, kw)
         if cfg_dup is not None:
             n = h.shape[0]
             if h.data_ptr() != cfg_dup.data_ptr():   # a plugin processor returned a new tensor
@@ -409,7 +450,7 @@ class UNet2DConditionModel(nn.Module):
     @torch.no_grad()
     def finalize(self) -> None:
         for m in self.modules():
-            if isinstance(m, (Attention, Transformer2DModel)):
+            if isinstance(m, (Attention, Transformer2DModel, BasicTransformerBlock)):
                 m.finalize()
         rs = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
         self.w_temb_all.copy_(torch.cat([r.time_emb_proj.weight for r in rs], 0))

@@ -37,6 +37,15 @@ extern "C" {
 #define C2D_PRO_GN 1         /* y = x*scale[n][c] + shift[n][c]  (GroupNorm affine, folded) */
 #define C2D_PRO_LN 2         /* y = (x-mean[m])*rstd[m]*gamma[c] + beta[c]                  */
 #define C2D_PRO_SILU 3       /* y = silu(x)                                                 */
+/* LayerNorm folded into a 1x1 GEMM whose K is the whole row (one source, c0 = kpad = 320 / 640,
+ * the panel GEMM): the kernel normalises each row of the A panel it holds in LDS in place,
+ * (x - mean) * rstd rounded to fp16 (eps = pro_eps), and runs the GEMM on it -- the
+ * LayerNorm(gamma, beta) -> Linear(W, b) pair with weight = W diag(gamma) (fp16) and
+ * bias = b + W beta (fp32).  pro_a / pro_b unused.  Act none or GEGLU, no residual / temb.
+ * Shapes the panel GEMM does not take: C2D_E_SHAPE.
+ * Replaces BasicTransformerBlock norm1 -> to_q/k/v and norm3 -> GEGLU (diffusers attention.py,
+ * reached from reference models/audio_attention_processor.py:115). */
+#define C2D_PRO_LNFOLD 4
 
 /* activation applied after the bias in the epilogue */
 #define C2D_ACT_NONE 0
@@ -98,6 +107,7 @@ typedef struct c2d_conv_desc {
                                 No prologue (pro must be C2D_PRO_NONE, else C2D_E_ARG): the
                                 border is read as data, so a GN / LN / SiLU would turn it into
                                 act(shift) instead of the zero padding torch applies        */
+    float pro_eps;           /* C2D_PRO_LNFOLD: the LayerNorm eps                         */
 } c2d_conv_desc;
 
 int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);

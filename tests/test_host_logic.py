@@ -107,3 +107,26 @@ def test_htsat_window_maps_match_roll_partition():
 def test_prompt_ids_deterministic():
     ids = prompt_to_ids("a beach")
     assert len(ids) == 77 and ids[0] == 49406 and ids[3] == 49407 and ids == prompt_to_ids("A beach")
+
+
+def test_fold_layernorm_algebra():
+    """ops.fold_layernorm: LayerNorm(gamma, beta) -> Linear(W, b) equals ((x - mean) * rstd) W'^T + b'
+    with W' = W diag(gamma), b' = b + W beta (the C2D_PRO_LNFOLD contract the panel GEMM
+    evaluates on its in-place normalised rows), up to W' rounding to fp16."""
+    import torch
+    from clap2diffusion_amd import ops
+    g = torch.Generator().manual_seed(7)
+    m, c, cout = 37, 320, 96
+    x = torch.randn(m, c, generator=g, dtype=torch.float64) * 3 + 50
+    gamma = 1 + 0.2 * torch.randn(c, generator=g, dtype=torch.float64)
+    beta = 0.2 * torch.randn(c, generator=g, dtype=torch.float64)
+    w = torch.randn(cout, c, generator=g) / c ** 0.5
+    b = 0.1 * torch.randn(cout, generator=g)
+    wp, kp = ops.pack_linear_weight(w)
+    wf, bf = ops.fold_layernorm(wp, b, gamma.float(), beta.float(), c)
+    assert wf.dtype == torch.float16 and wf.shape == wp.shape and bf.shape == (cout,)
+    mean = x.mean(1, keepdim=True)
+    rstd = 1 / torch.sqrt(x.var(1, unbiased=False, keepdim=True) + 1e-5)
+    fold = ((x - mean) * rstd) @ wf[:, :c].double().t() + bf.double().view(1, -1)
+    ref = torch.nn.functional.layer_norm(x, (c,), gamma, beta, 1e-5) @ wp[:, :c].double().t() + b.double()
+    assert ((fold - ref).abs().max() / ref.abs().max()).item() < 2e-3

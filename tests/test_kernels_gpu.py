@@ -412,6 +412,37 @@ def test_panel_gemm_forced_geglu(dev, force_plan, m, cin, inner):
     close(out, ref)
 
 
+@pytest.mark.parametrize("m,c,cout,geglu,mean", [
+    (4096, 320, 960, False, 0.0), (2048, 320, 2560, True, 0.0),      # fused QKV / GEGLU of level 0
+    (1000, 320, 960, False, 40.0), (300, 320, 2560, True, -25.0),    # ragged last panel, |row mean| >> std
+    (2048, 640, 5120, True, 0.0), (700, 640, 1920, False, 30.0),     # level 1 (the register-ring panel kernel)
+])
+def test_panel_gemm_layernorm_fold(dev, m, c, cout, geglu, mean):
+    """LayerNorm folded into the panel GEMM (C2D_PRO_LNFOLD, igemm_panel_dma_kernel LNF: the
+    LDS panel normalised in place, then W diag(gamma) with bias b + W beta) against torch's
+    LayerNorm -> Linear (diffusers BasicTransformerBlock norm1 -> to_q/k/v, norm3 -> GEGLU);
+    rows offset by up to +-30 on top of `mean` (|mean| >> std: the shifted second pass)."""
+    x = gen(m, c, seed=110) + mean + gen(m, 1, seed=111) * 30.0
+    gamma, beta = 1.0 + 0.2 * gen(c, seed=112), 0.2 * gen(c, seed=113)
+    w = gen(cout, c, seed=114, scale=1.0 / math.sqrt(c))
+    b = 0.1 * gen(cout, seed=115)
+    xh = x.half()
+    y = F.layer_norm(xh.float(), (c,), gamma, beta, 1e-5) @ w.t() + b
+    if geglu:
+        hh, gg = y.chunk(2, -1)
+        ref = hh * F.gelu(gg)
+        w, b = ops.geglu_interleave(w, b)
+    else:
+        ref = y
+    wp, kp = ops.pack_linear_weight(w)
+    wf, bf = ops.fold_layernorm(wp, b, gamma, beta, c)
+    with ops.record_conv_plans() as plans:
+        out = ops.conv(xh.to(dev), wf.to(dev), kp, cout, ksize=1, bias=bf.to(dev), act="geglu" if geglu else None,
+                       ln_fold=1e-5)
+    assert plans == [(70, 1)], plans
+    close(out, ref)
+
+
 def test_panel_gemm_ineligible_falls_back(dev, force_plan):
     """Forcing tile 70 on a shape it does not take (K = 1280) leaves the planner's choice."""
     force_plan(70, 0)
