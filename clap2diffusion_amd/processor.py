@@ -93,10 +93,10 @@ class AttnProcessor(nn.Module):
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
                  scale: float = 1.0, _residual: Optional[torch.Tensor] = None, _qkv: Optional[torch.Tensor] = None,
-                 **cross_attention_kwargs):
-        """_qkv: the self-attention's [B*L, 3*inner] projections already computed by the caller
-        (BasicTransformerBlock: norm1 folded into the QKV GEMM); hidden_states then only gives
-        the shape."""
+                 _q: Optional[torch.Tensor] = None, **cross_attention_kwargs):
+        """_qkv / _q: the self-attention's [B*L, 3*inner] / the cross-attention's [B*L, inner]
+        projections already computed by the caller (BasicTransformerBlock: norm1 / norm2 folded into
+        the GEMM); hidden_states then only gives the shape."""
         x, restore = _as_tokens(hidden_states)
         b, l, c = x.shape
         x2 = x.view(b * l, c)
@@ -114,7 +114,7 @@ class AttnProcessor(nn.Module):
             if kv is None:
                 kv = AttnProcessor.context_kv(self, attn, encoder_hidden_states)
             lk = kv.shape[0] // b
-            q = ops.conv(x2, attn.to_q.weight, attn.kpad_q, inner, ksize=1)
+            q = _q if _q is not None else ops.conv(x2, attn.to_q.weight, attn.kpad_q, inner, ksize=1)
             if scale != 1.0:
                 q.mul_(scale)
             o = ops.attention(q, kv[:, :inner], kv[:, inner:], b, heads, l, lk, d,
@@ -211,13 +211,16 @@ class AudioAttnProcessor(nn.Module):
         return kv.view(b * lk, 2 * inner)
 
     def __call__(self, attn, hidden_states, encoder_hidden_states=None, attention_mask=None, temb=None,
-                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, **cross_attention_kwargs):
+                 scale: float = 1.0, _residual: Optional[torch.Tensor] = None, _q: Optional[torch.Tensor] = None,
+                 **cross_attention_kwargs):
+        """_q: to_q(hidden_states) already computed by the caller (BasicTransformerBlock: norm2
+        folded into the to_q GEMM); hidden_states then only gives the shape."""
         x, restore = _as_tokens(hidden_states)
         b, l, c = x.shape
         heads, d = attn.heads, attn.dim_head
         inner = heads * d
         ehs = encoder_hidden_states
-        q = ops.conv(x.view(b * l, c), attn.to_q.weight, attn.kpad_q, inner, ksize=1)
+        q = _q if _q is not None else ops.conv(x.view(b * l, c), attn.to_q.weight, attn.kpad_q, inner, ksize=1)
         if scale != 1.0:
             q.mul_(scale)
         if ehs is None:

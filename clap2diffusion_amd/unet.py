@@ -43,7 +43,7 @@ import torch.nn as nn
 
 from . import ops
 from .layers import HConv2d, HGroupNorm, HLayerNorm, HLinear
-from .processor import AttnProcessor
+from .processor import AttnProcessor, AudioAttnProcessor
 from .weights import SD15_UNET
 
 # ff.net.2 folded into proj_out (Transformer2DModel): read once at import, A/B switch only
@@ -147,11 +147,11 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim)
         # LayerNorm folded into the GEMM after it (C2D_PRO_LNFOLD, the panel GEMM's K = 320 / 640: the
         # kernel normalises its LDS panel in place): W diag(gamma) and b + W beta for norm1 -> fused
-        # QKV and norm3 -> GEGLU (finalize); used where the planner runs those GEMMs on the panel kernel
+        # QKV, norm2 -> to_q and norm3 -> GEGLU (finalize); used where _lnf_on says so
         self.lnf = dim in (320, 640)
         inner = self.attn1.heads * self.attn1.dim_head
         kp = self.attn1.kpad_q
-        for name, rows in (("qkv", 3 * inner), ("ff", self.ff.net[0].proj.out_features)):
+        for name, rows in (("qkv", 3 * inner), ("q", inner), ("ff", self.ff.net[0].proj.out_features)):
             self.register_buffer(f"lnf_{name}_w", torch.zeros(rows, kp, dtype=torch.float16) if self.lnf else None,
                                  persistent=False)
             self.register_buffer(f"lnf_{name}_b", torch.zeros(rows) if self.lnf else None, persistent=False)
@@ -162,14 +162,19 @@ class BasicTransformerBlock(nn.Module):
             return
         c = self.norm1.c
         wq = torch.cat([self.attn1.to_q.weight, self.attn1.to_k.weight, self.attn1.to_v.weight], 0)
-        for name, w, b, norm in (("qkv", wq, None, self.norm1),
+        for name, w, b, norm in (("qkv", wq, None, self.norm1), ("q", self.attn2.to_q.weight, None, self.norm2),
                                  ("ff", self.ff.net[0].proj.weight, self.ff.net[0].proj.bias, self.norm3)):
             wf, bf = ops.fold_layernorm(w, b, norm.weight, norm.bias, c)
             getattr(self, f"lnf_{name}_w").copy_(wf)
             getattr(self, f"lnf_{name}_b").copy_(bf)
 
     def _lnf_on(self, m: int, cout: int, geglu: bool) -> bool:
-        return FOLD_LN and self.lnf and ops.panel_gemm(m, self.norm1.c, cout, geglu)
+        """Fold the LayerNorm into this GEMM: where the planner runs it on the panel kernel anyway,
+        and at K = 320 from 8192 rows on, where the folded panel GEMM beats LayerNorm + the
+        planner's tile on every UNet shape measured (profiles/r05_ln_fold.txt: to_q 320 -> 320 at
+        c3 42.8 -> 34.7 us, c5's fused QKV 105.9 -> 92.4); at K = 640 only the panel shapes gain."""
+        c = self.norm1.c
+        return FOLD_LN and self.lnf and (ops.panel_gemm(m, c, cout, geglu) or (c == 320 and m >= 8192))
 
     def _attend(self, attn: Attention, x, h, ehs, mask, kwargs):
         if getattr(attn.processor, "fuses_residual", False):
@@ -224,6 +229,12 @@ class BasicTransformerBlock(nn.Module):
                 cfg_dup[:n].copy_(h)
             cfg_dup[n:].copy_(cfg_dup[:n])
             h = cfg_dup
+        b, l, c = h.shape
+        if type(self.attn2.processor) in (AttnProcessor, AudioAttnProcessor) and self._lnf_on(b * l, inner, False):
+            # norm2 folded into to_q; the stock / audio processor takes the projected query
+            q = ops.conv(h.view(b * l, c), self.lnf_q_w, self.attn2.kpad_q, inner, ksize=1, bias=self.lnf_q_b,
+                         ln_fold=self.norm2.eps)
+            return self._attend(self.attn2, h, h, ehs, encoder_attention_mask, dict(kw, _q=q))
         return self._attend(self.attn2, self.norm2(h), h, ehs, encoder_attention_mask, kw)
 
 
