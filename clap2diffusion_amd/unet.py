@@ -18,14 +18,20 @@ blocks, GN+SiLU+conv_out.  Fusions on the HIP path:
   Block           LN1 -> fused QKV GEMM -> flash attn -> to_out (+residual);
                   LN2 -> audio cross-attn processor (+residual);
                   LN3 -> GEGLU GEMM (h*gelu(g) epilogue) -> Linear (+residual).
+  LayerNorm fold  LN1 / LN2 / LN3 run inside the QKV / to_q / GEGLU GEMM where that GEMM is the
+                  panel kernel (K = 320 from 8192 rows, K = 640 on its planned shapes): the
+                  workgroup normalises its LDS-resident A panel in place and multiplies by
+                  W diag(gamma) with bias b + W beta (C2D_PRO_LNFOLD; BasicTransformerBlock._lnf_on;
+                  C2D_LN_FOLD=0 materialises the LayerNorm outputs).
   FF out fold     ff.net.2 and proj_out are two linear maps with only a residual add
                   between them: proj_out(h + W2 g + b2) + x = [Wp | Wp W2] [h; g] +
                   (Wp b2 + bp) + x, one K = 5C GEMM reading h and g from their own
                   buffers (Transformer2DModel.finalize / forward; C2D_FOLD_FF_OUT=0
                   keeps the two GEMMs).
-  Normalised activations are materialised once per norm (HBM-bound kernels):
+  Other normalised activations (GroupNorm) are materialised once per norm (HBM-bound kernels):
   re-normalising inside the consumer GEMM would redo the affine+SiLU in all 9
-  taps of a 3x3 conv / every N-tile of a GEMM, which is VALU-bound on CDNA4.
+  taps of a 3x3 conv / every N-tile of a GEMM, which is VALU-bound on CDNA4 -- the panel GEMM
+  escapes that because it normalises each A row once, in LDS, for all of its output columns.
   Up/Downsample   stride 2 folded into the conv addressing; the nearest x2 upsample
                   materialised by c2d_upsample_nearest2x (one HBM pass) so the 3x3 conv
                   stays on the LDS-DMA path (Upsample2D below).
