@@ -112,6 +112,24 @@ int main() {
         d.pro = C2D_PRO_SILU; d.pro_a = nullptr; d.pro_b = nullptr;
         CHECK(c2d_conv2d_igemm(&d, nullptr) == C2D_E_ARG);
     }
+    {
+        // a folded LayerNorm (C2D_PRO_LNFOLD): the panel GEMM (1x1, K = 320 / 640) or C2D_E_SHAPE, eps > 0
+        c2d_conv_desc d = desc(1, 1, 4096, 320, 0, 1, 1, 960, C2D_ACT_NONE);
+        d.pro = C2D_PRO_LNFOLD; d.pro_eps = 1e-5f;
+        int tile = -1, split = -1;
+        CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK && tile == 70 && split == 1);
+        CHECK(c2d_conv2d_igemm_workspace_size(&d) == 0);
+        c2d_conv_desc g = desc(1, 1, 2048, 640, 0, 1, 1, 5120, C2D_ACT_GEGLU);
+        g.pro = C2D_PRO_LNFOLD; g.pro_eps = 1e-5f;
+        CHECK(c2d_conv2d_igemm_plan(&g, &tile, &split) == C2D_OK && tile == 70);
+        c2d_conv_desc e = d; e.pro_eps = 0.f;             CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_ARG);
+        e = desc(1, 1, 4096, 1280, 0, 1, 1, 640, C2D_ACT_NONE);
+        e.pro = C2D_PRO_LNFOLD; e.pro_eps = 1e-5f;        CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        CHECK(c2d_conv2d_igemm_plan(&e, &tile, &split) == C2D_E_SHAPE);
+        e = desc(16, 64, 64, 320, 0, 3, 1, 320, C2D_ACT_NONE);   // a 3x3 conv has no whole-row K
+        e.pro = C2D_PRO_LNFOLD; e.pro_eps = 1e-5f;        CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        e = d; e.resid = d.out; e.resid_ld = 960;         CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+    }
     for (int nb : {1, 2, 8})                                            // VAE decoder
         for (int hw : {64, 128, 256, 512})
             for (int c : {128, 256, 512}) check_plan(desc(nb, hw, hw, c, 0, 3, 1, c, C2D_ACT_NONE));
