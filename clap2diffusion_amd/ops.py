@@ -141,18 +141,21 @@ def fold_layernorm(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch
 
 
 @functools.lru_cache(maxsize=None)
-def panel_gemm(m: int, k: int, cout: int, geglu: bool) -> bool:
+def panel_gemm(m: int, k: int, cout: int, geglu: bool, lnfold: bool = False) -> bool:
     """Does c2d's planner run this 1x1 GEMM (m x k -> cout) on the panel GEMM (tile 70)?  Where it
-    does, a LayerNorm before it folds in (C2D_PRO_LNFOLD)."""
+    does, a LayerNorm before it folds in.  lnfold: would the library take this GEMM with a folded
+    LayerNorm (C2D_PRO_LNFOLD: the panel GEMM's shapes and switches, else C2D_E_SHAPE)?"""
     import ctypes
-    from ._lib import ConvDesc, check, lib
+    from ._lib import C2D_PRO_LNFOLD, ConvDesc, lib
     d = ConvDesc()
     d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride = k, 1, 1, m, 1, m, 1, 1
     d.cout, d.kpad, d.act = cout, kpad_of(k), C2D_ACT["geglu" if geglu else None]
     d.out_ld = cout // 2 if geglu else cout
+    if lnfold:
+        d.pro, d.pro_eps = C2D_PRO_LNFOLD, 1e-5
     tid, ks = ctypes.c_int(), ctypes.c_int()
-    check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
-    return tid.value == 70
+    rc = lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks))
+    return rc == 0 and tid.value == 70
 
 
 @functools.lru_cache(maxsize=None)

@@ -180,7 +180,8 @@ class BasicTransformerBlock(nn.Module):
         planner's tile on every UNet shape measured (profiles/r05_ln_fold.txt: to_q 320 -> 320 at
         c3 42.8 -> 34.7 us, c5's fused QKV 105.9 -> 92.4); at K = 640 only the panel shapes gain."""
         c = self.norm1.c
-        return FOLD_LN and self.lnf and (ops.panel_gemm(m, c, cout, geglu) or (c == 320 and m >= 8192))
+        return (FOLD_LN and self.lnf and ops.panel_gemm(m, c, cout, geglu, lnfold=True)
+                and (ops.panel_gemm(m, c, cout, geglu) or (c == 320 and m >= 8192)))
 
     def _attend(self, attn: Attention, x, h, ehs, mask, kwargs):
         if getattr(attn.processor, "fuses_residual", False):
