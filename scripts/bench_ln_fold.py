@@ -2,7 +2,7 @@
 the UNet's norm1 -> fused QKV and norm3 -> GEGLU shapes at c3 (M = 65536; level 1: 16384 x 640),
 c2 (8192), c5 (73728).
 
-python scripts/bench_ln_fold.py [--all]"""
+python scripts/bench_ln_fold.py [--all | --extra]"""
 import math
 import sys
 from pathlib import Path
@@ -37,7 +37,10 @@ def timed(fn, reps=20):
 
 
 ALL = "--all" in sys.argv   # also shapes the planner keeps off the panel GEMM (the fold forces it)
-for m, c in ((65536, 320), (8192, 320), (73728, 320), (16384, 640), (2048, 640)):
+SHAPES = ((65536, 320), (8192, 320), (73728, 320), (16384, 640), (2048, 640))
+if "--extra" in sys.argv:   # c5's level 1 (8 x 48^2 rows) and c2's CFG-shared half batch
+    SHAPES, ALL = ((18432, 640), (4096, 320)), True
+for m, c in SHAPES:
     for cout, geglu in ((3 * c, False), (8 * c, True), (c, False)):
         if not (ALL or ops.panel_gemm(m, c, cout, geglu)):
             continue
