@@ -724,16 +724,16 @@ __global__ void __launch_bounds__(256) attn_pp_kernel(const f16* __restrict__ q,
 #undef KB
 #undef VB
 
-// C2D_ATTN_PP=1 selects the double-buffered, software-pipelined d=40 kernel.  Measured
+// C2D_TUNE_ATTN_PP=1 (variant build) selects the double-buffered, software-pipelined d=40 kernel.  Measured
 // slower than the single-buffered one on MI355X (L0 self 4096x4096: 779 vs 653 us): the
 // in-flight S tile takes it to 148 VGPR + 24 AGPR = 2 waves/SIMD vs 126 + 40 = 3 for
 // attn_fwd_kernel<40>, and the doubled K/V ring halves the blocks LDS admits, so it is
 // off by default.
-// A/B switches, read once (runtime.hip tuning()): C2D_ATTN_ABL (ablation builds only:
-// K/V staging skipped), C2D_ATTN_NEGC=0 (fma-per-score softmax), C2D_ATTN_RES=0 (stream
-// K/V tiles for short key sequences too), C2D_ATTN_W8=0 (4-wave d = 40 blocks),
-// C2D_ATTN_PP=1 (the pipelined d = 40 kernel above)
-static int attn_abl() { return tuning().attn_abl; }
+// A/B constants (common.h, variant builds): C2D_TUNE_ATTN_NEGC=0 (fma-per-score softmax),
+// C2D_TUNE_ATTN_RES=0 (stream K/V tiles for short key sequences too), C2D_TUNE_ATTN_W8=0
+// (4-wave d = 40 blocks), C2D_TUNE_ATTN_PP=1 (the pipelined d = 40 kernel above); the timing
+// ablation C2D_ATTN_ABL (K/V staging skipped) exists in the ablation build only
+static int attn_abl() { return ablation_attn(); }
 static bool attn_negc() { return tuning().attn_negc != 0; }
 static bool attn_res() { return tuning().attn_res != 0; }
 static bool attn_w8() { return tuning().attn_w8 != 0; }

@@ -49,14 +49,79 @@ __device__ __forceinline__ void static_for(F&& f) {
 // thread-local last launch error, exposed as c2d_last_hip_error() (runtime.hip)
 extern thread_local int g_last_hip_error;
 
-// Tuning switches (A/B only; defaults are the measured best), read from the environment
-// once per process under std::call_once (runtime.hip) and immutable afterwards.
+// Tuning constants (A/B only; the defaults are the measured best).  Compile-time: an A/B
+// candidate is a variant build (python -m clap2diffusion_amd.build --variant x --define
+// C2D_TUNE_GN_FOLD=0, loaded through C2D_LIB), so the production library reads no
+// environment variable and cannot be switched to another kernel or numerics at run time.
+#ifndef C2D_TUNE_GEMM_MODE
+#define C2D_TUNE_GEMM_MODE 0        // 2: register-staged kernels only
+#endif
+#ifndef C2D_TUNE_GEMM_KORDER
+#define C2D_TUNE_GEMM_KORDER 1      // 3x3 K order: channel-block outer (1) / tap outer (0)
+#endif
+#ifndef C2D_TUNE_GEMM_LDSEPI
+#define C2D_TUNE_GEMM_LDSEPI 1      // 0: direct 32x32 GEGLU epilogue
+#endif
+#ifndef C2D_TUNE_SPLITK_F16
+#define C2D_TUNE_SPLITK_F16 0       // 1: split-K partials in fp16 (cancelling partials lose range / precision)
+#endif
+#ifndef C2D_TUNE_TAIL_SPLIT
+#define C2D_TUNE_TAIL_SPLIT 1       // 0: no image split of a quantisation tail
+#endif
+#ifndef C2D_TUNE_PANEL_REGB
+#define C2D_TUNE_PANEL_REGB 0       // 1: the K = 320 panel GEMM loads its weights into registers
+#endif
+#ifndef C2D_TUNE_PANEL_STAGGER
+#define C2D_TUNE_PANEL_STAGGER 2    // panel GEMM: late start of waves 4-7, x 2048 cycles
+#endif
+#ifndef C2D_TUNE_ATTN_NEGC
+#define C2D_TUNE_ATTN_NEGC 1
+#endif
+#ifndef C2D_TUNE_ATTN_RES
+#define C2D_TUNE_ATTN_RES 1
+#endif
+#ifndef C2D_TUNE_ATTN_W8
+#define C2D_TUNE_ATTN_W8 1
+#endif
+#ifndef C2D_TUNE_ATTN_PP
+#define C2D_TUNE_ATTN_PP 0
+#endif
+#ifndef C2D_TUNE_GN_BLOCKS
+#define C2D_TUNE_GN_BLOCKS 512
+#endif
+#ifndef C2D_TUNE_GN_APPLY_BLOCKS
+#define C2D_TUNE_GN_APPLY_BLOCKS 2048
+#endif
+#ifndef C2D_TUNE_GN_FUSED_HW
+#define C2D_TUNE_GN_FUSED_HW 256
+#endif
+#ifndef C2D_TUNE_GN_FOLD
+#define C2D_TUNE_GN_FOLD 1          // 0: partial + finalize + apply
+#endif
+#ifndef C2D_TUNE_GN_FOLD_CAP
+#define C2D_TUNE_GN_FOLD_CAP 32     // most partial blocks per image on the fold path
+#endif
+#ifndef C2D_TUNE_GN_FOLD_APPLY_BLOCKS
+#define C2D_TUNE_GN_FOLD_APPLY_BLOCKS 1024   // apply workgroups per launch (fold path, batches below 8 images)
+#endif
 struct Tuning {
-    int gemm_mode, gemm_korder, gemm_lds_epi, gemm_abl, splitk_f16, tail_split, gemm_sp, panel_regb, panel_stagger;
-    int attn_negc, attn_res, attn_w8, attn_pp, attn_abl;
+    int gemm_mode, gemm_korder, gemm_lds_epi, splitk_f16, tail_split, panel_regb, panel_stagger;
+    int attn_negc, attn_res, attn_w8, attn_pp;
     int gn_blocks, gn_apply_blocks, gn_fused_hw, gn_fold, gn_fold_cap, gn_fold_apply_blocks;
 };
-const Tuning& tuning();
+constexpr Tuning kTuning = {
+    C2D_TUNE_GEMM_MODE, C2D_TUNE_GEMM_KORDER, C2D_TUNE_GEMM_LDSEPI, C2D_TUNE_SPLITK_F16, C2D_TUNE_TAIL_SPLIT,
+    C2D_TUNE_PANEL_REGB, C2D_TUNE_PANEL_STAGGER,
+    C2D_TUNE_ATTN_NEGC, C2D_TUNE_ATTN_RES, C2D_TUNE_ATTN_W8, C2D_TUNE_ATTN_PP,
+    C2D_TUNE_GN_BLOCKS < 64 ? 512 : C2D_TUNE_GN_BLOCKS, C2D_TUNE_GN_APPLY_BLOCKS < 64 ? 2048 : C2D_TUNE_GN_APPLY_BLOCKS,
+    C2D_TUNE_GN_FUSED_HW, C2D_TUNE_GN_FOLD, C2D_TUNE_GN_FOLD_CAP < 1 ? 32 : C2D_TUNE_GN_FOLD_CAP,
+    C2D_TUNE_GN_FOLD_APPLY_BLOCKS < 64 ? 1024 : C2D_TUNE_GN_FOLD_APPLY_BLOCKS,
+};
+constexpr const Tuning& tuning() { return kTuning; }
+// timing-ablation masks: C2D_GEMM_ABL / C2D_ATTN_ABL read from the environment in the
+// -DC2D_ENABLE_ABLATION build only (runtime.hip); 0 in the production library
+int ablation_gemm();
+int ablation_attn();
 // c2d_set_plan_override (tests / sweeps): 0 = the planner decides
 int plan_override_tile();
 int plan_override_split();

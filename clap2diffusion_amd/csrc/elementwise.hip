@@ -207,7 +207,7 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, int cout, int c
 
 using namespace c2d;
 
-extern "C" const char* c2d_version(void) { return "c2d_hip gfx950 r3"; }
+extern "C" const char* c2d_version(void) { return "c2d_hip gfx950 r6"; }
 
 extern "C" int c2d_timestep_embedding(const float* t_table, const int* step_index, int n, int dim, void* out,
                                       void* stream) {

@@ -52,10 +52,10 @@ struct IgemmParams {
     int ksplit;  // K slices per output tile (DMA path; 1 = no split)
     int nkt;     // K steps per slice
     float* ws;   // split-K partials [ksplit][M][cout]: fp32, or fp16 when slab16
-    int slab16;  // split-K partials stored as fp16 (C2D_SPLITK_F16): half the slab write + combine read
+    int slab16;  // split-K partials stored as fp16 (C2D_TUNE_SPLITK_F16): half the slab write + combine read
     int abl;     // timing ablation bits (C2D_GEMM_ABL; 0 in production)
-    int lds_epi; // 32x32 kernels: 1 = LDS-staged epilogue (C2D_GEMM_LDSEPI or alignment), 0 = direct
-    int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_GEMM_KORDER, default 1)
+    int lds_epi; // 32x32 kernels: 1 = LDS-staged epilogue (C2D_TUNE_GEMM_LDSEPI or alignment), 0 = direct
+    int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_TUNE_GEMM_KORDER, default 1)
     float pro_eps;   // C2D_PRO_LNFOLD: LayerNorm eps
 };
 
@@ -745,8 +745,6 @@ void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #include "igemm_pp16.h"
 #include "igemm_pps.h"
 #include "igemm_pp16r.h"
-#include "igemm_sp.h"
-#include "igemm_spr.h"
 #include "igemm_panel.h"
 namespace c2d {
 
@@ -775,8 +773,8 @@ static void launch(const IgemmParams& p, hipStream_t s) {
 
 using namespace c2d;
 
-// C2D_GEMM_MODE=2 restricts to the register-staged kernels (A/B comparisons,
-// debugging); default 0 = auto.  Read once (runtime.hip tuning()).
+// C2D_TUNE_GEMM_MODE=2 (variant build) restricts to the register-staged kernels (A/B
+// comparisons, debugging); default 0 = auto.
 static int gemm_mode() { return tuning().gemm_mode; }
 
 // c2d_set_plan_override(tile, split): force DMA tile config `tile` (shape sweeps, the
@@ -797,24 +795,12 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
-C2D_TILE_FN(42); C2D_TILE_FN(60); C2D_TILE_FN(61); C2D_TILE_FN(62); C2D_TILE_FN(70);
+C2D_TILE_FN(42); C2D_TILE_FN(70);
 #if C2D_PART(1)
-#ifdef C2D_SP_STAMP
-}  // namespace c2d
-// diagnostic variant only (not in c2d.h): copy the stamps of the last stamped launch to host memory
-extern "C" int c2d_debug_sp_stamps(unsigned long long* host, int n) {
-    if (n > 8 * c2d::kStampPer) n = 8 * c2d::kStampPer;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(c2d::g_sp_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -4;
-}
-namespace c2d {
-#endif
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
 C2D_TILE_FN(50) { (void)ksize; (void)cout; run_pps(p, s); }   // persistent 192x256, carried epilogue (1x1)
 C2D_TILE_FN(42) { (void)ksize; (void)cout; run_pp16r<5>(p, s); }   // 256x320 row-ring 3x3 over a zero-bordered source
-C2D_TILE_FN(60) { run_sp<5>(p, ksize, cout, s); }   // 256x320 software-pipelined, two barriers per K step
-C2D_TILE_FN(61) { run_sp<4>(p, ksize, cout, s); }   // 256x256 software-pipelined
-C2D_TILE_FN(62) { (void)ksize; (void)cout; run_spr<5>(p, s); }   // 256x320 row-ring software-pipelined 3x3
 #endif
 #if C2D_PART(2)
 C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
@@ -860,10 +846,6 @@ static const DmaTile kDmaTiles[] = {
     {9, 64, 160, 2, 0.0f, false},
     // row-ring 3x3 over a zero-bordered source (igemm_pp16r.h): chosen by plan_for only
     {42, 256, 320, 1, 0.0f, false},
-    // software-pipelined twins of 40 / 41 (igemm_sp.h): one barrier per K step
-    {60, 256, 320, 1, 0.0f, false},
-    {61, 256, 256, 1, 0.0f, true},
-    {62, 256, 320, 1, 0.0f, false},   // row-ring twin of 42 (igemm_spr.h): chosen like 42, never by plan_dma
 };
 struct DmaPlan { int id, split, nkt; };
 
@@ -896,7 +878,7 @@ static DmaPlan plan_dma(long M, int cout, int nk, bool geglu, int force_id, int 
 
 // C2D_GEMM_ABL: timing ablation of the DMA kernels (1 = no DMA, 2 = no MFMA; m32: 4 = no epilogue,
 // 8 = with 2, no fragment reads either); wrong results by design, so only in -DC2D_ENABLE_ABLATION builds
-static int gemm_abl() { return tuning().gemm_abl; }
+static int gemm_abl() { return ablation_gemm(); }
 
 // K-step order of the 3x3 DMA kernels.  1 (default): for each 64-channel block all
 // 9 taps, so one block re-reads a (rows + 2 halo image rows) x 64-channel slab from
@@ -905,7 +887,7 @@ static int gemm_abl() { return tuning().gemm_abl; }
 // the 4 MB L2 at cin = 320 and re-fetches the input over the fabric once per tap.
 static int gemm_korder() { return tuning().gemm_korder; }
 
-// C2D_GEMM_LDSEPI=0 lets the 32x32 GEGLU GEMMs store straight from the accumulators:
+// C2D_TUNE_GEMM_LDSEPI=0 (variant build) lets the 32x32 GEGLU GEMMs store straight from the accumulators:
 // 10 % faster in isolation (L0 320 -> 2 x 1280) but 0.3 % slower in the full step
 // (same-box bench A/B, twice each), so the LDS-staged epilogue stays the default
 static int gemm_lds_epi() { return tuning().gemm_lds_epi; }
@@ -1025,12 +1007,8 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
         if (panel_ok && gemm_split() <= 1) return {70, 1, nk};
         id = 0;
     }
-    if (id == 42 || id == 62) {
-        if (rr_ok) {
-            DmaPlan pl = rr_plan(nk, gemm_split());
-            pl.id = id;
-            return pl;
-        }
+    if (id == 42) {
+        if (rr_ok) return rr_plan(nk, gemm_split());
         id = 0;
     }
     // the row-ring 3x3 (tile 42) on a zero-bordered source once its 256 x 320 tiles fill the chip
@@ -1106,14 +1084,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
 static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout, hipStream_t s) {
     p.ksplit = pl.split;
     p.nkt = pl.nkt;
-    int id = pl.id;
-    if (tuning().gemm_sp && id == 40) id = 60;   // C2D_GEMM_SP: the software-pipelined twins (A/B)
-    if (tuning().gemm_sp && id == 41) id = 61;
-    if (tuning().gemm_sp && id == 42) id = 62;
-    switch (id) {
-        case 60: return run_tile_60(p, ksize, cout, s);
-        case 61: return run_tile_61(p, ksize, cout, s);
-        case 62: return run_tile_62(p, ksize, cout, s);
+    switch (pl.id) {
         case 42: return run_tile_42(p, ksize, cout, s);
         case 25: return run_tile_25(p, ksize, cout, s);
         case 40: return run_tile_40(p, ksize, cout, s);
@@ -1216,14 +1187,14 @@ extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
 extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit) {
     if (!d || !tile_id || !ksplit) return C2D_E_ARG;
     if (d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return C2D_E_SHAPE;
-    if (!dma_eligible(d)) {
-        *tile_id = 0;
+    if (d->pro == C2D_PRO_LNFOLD) {   // the panel GEMM or nothing (c2d_conv2d_igemm rejects the rest the same way)
+        if (!panel_eligible(d)) return C2D_E_SHAPE;
+        *tile_id = 70;
         *ksplit = 1;
         return C2D_OK;
     }
-    if (d->pro == C2D_PRO_LNFOLD) {   // the panel GEMM or nothing
-        if (!panel_eligible(d)) return C2D_E_SHAPE;
-        *tile_id = 70;
+    if (!dma_eligible(d)) {
+        *tile_id = 0;
         *ksplit = 1;
         return C2D_OK;
     }
@@ -1280,7 +1251,7 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     if (d->pro == C2D_PRO_GN && (!d->pro_a || !d->pro_b || (cin & 3))) return C2D_E_ARG;
     if (d->pro == C2D_PRO_LN && (!d->pro_a || !d->gamma || !d->beta)) return C2D_E_ARG;
     if (d->pro < 0 || d->pro > 4 || d->act < 0 || d->act > 5) return C2D_E_ARG;
-    if (d->pro == C2D_PRO_LNFOLD && !(d->pro_eps > 0.f)) return C2D_E_ARG;
+    if (d->pro == C2D_PRO_LNFOLD && !(d->pro_eps > 0.f)) return C2D_E_ARG;   // pro_eps: read only for LNFOLD
     if (d->pro == C2D_PRO_LNFOLD && !panel_eligible(d)) return C2D_E_SHAPE;   // only the panel GEMM folds LN
     if (d->stride != 1 && d->stride != 2) return C2D_E_SHAPE;
     if (d->ksize == 1 && (d->stride != 1 || d->up || d->oh != d->h || d->ow != d->w)) return C2D_E_SHAPE;
@@ -1307,7 +1278,7 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     p.pro = d->pro; p.pro_silu = d->pro_silu;
     p.pro_a = d->pro_a; p.pro_b = d->pro_b; p.gamma = d->gamma; p.beta = d->beta;
     p.bias = d->bias; p.act = d->act;
-    p.pro_eps = d->pro_eps;
+    p.pro_eps = d->pro == C2D_PRO_LNFOLD ? d->pro_eps : 0.f;   // the r5 field: read only when it applies
     p.temb = (const f16*)d->temb; p.temb_ld = d->temb_ld;
     p.resid = (const f16*)d->resid; p.resid_ld = d->resid_ld;
     p.out = (f16*)d->out; p.out_ld = d->out_ld;

@@ -168,7 +168,7 @@ struct M32Loader {
         }
     }
     __device__ __forceinline__ void advance() {
-        if (KS == 3 && cbase_major) {                     // taps inner (C2D_GEMM_KORDER)
+        if (KS == 3 && cbase_major) {                     // taps inner (C2D_TUNE_GEMM_KORDER)
             if (++tap == 9) { tap = 0; cbase += BK; }
         } else {
             cbase += BK;
@@ -548,7 +548,7 @@ static void launch_m32(const IgemmParams& p, hipStream_t s) {
 
 template <int WM, int WN, int TM, int TN, int BK, int ST, int DB, int KS, int WPE, bool DIRECT>
 static void launch_m32_act(const IgemmParams& p, hipStream_t s) {
-    // direct only for GEGLU (and only with C2D_GEMM_LDSEPI=0): plain outputs are
+    // direct only for GEGLU (and only with C2D_TUNE_GEMM_LDSEPI=0): plain outputs are
     // faster through the LDS image (its 16-B coalesced stores beat the 8-B row
     // pieces: L0 qkv 69.5 vs 78.8 us); GEGLU alone is faster direct (L0 320 -> 2 x
     // 1280: 170 vs 190 us) but not inside the full step

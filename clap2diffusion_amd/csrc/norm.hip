@@ -716,13 +716,13 @@ static int ln_dispatch(const void* x, int m, int c, int ld, float eps, float* st
 
 using namespace c2d;
 
-// target partial-block count of a launch (C2D_GN_BLOCKS, A/B only).  512: 64^2 x 320 GN
+// target partial-block count of a launch (C2D_TUNE_GN_BLOCKS, A/B only).  512: 64^2 x 320 GN
 // 30.5 -> 29.3 us, 32^2 x 640 23.4 -> 20.6 us vs 1024 (graph-replayed, same box; 2048 slower)
 static int gn_target_blocks() { return tuning().gn_blocks; }
 
 // rows (pixels) per partial block: about gn_target_blocks() blocks over the whole launch,
 // at least one full pass of the block's row-threads, at most 128
-// apply workgroups per launch (C2D_GN_APPLY_BLOCKS, A/B only; default 2048)
+// apply workgroups per launch (C2D_TUNE_GN_APPLY_BLOCKS, A/B only; default 2048)
 static int gn_apply_blocks() { return tuning().gn_apply_blocks; }
 
 // rows per partial block: about gn_target_blocks() blocks over the launch, but at most
@@ -832,7 +832,7 @@ static int gn_fused_cb(int n, int cin, int groups) {
     return cb;
 }
 
-// pixels per image up to which the single-launch kernel is used (C2D_GN_FUSED_HW).
+// pixels per image up to which the single-launch kernel is used (C2D_TUNE_GN_FUSED_HW).
 // Graph-replayed per call at N = 16 (scripts/bench_norm_graph.py): 8^2 x 1280
 // 16.8 -> 6.2 us, 16^2 x 1280 21.3 -> 13.0 us, but 32^2 x 640 23.1 -> 26.6 us
 // (40-channel chunks read 80-B row pieces over 1024 pixels) and 64^2 2-5x slower.
@@ -844,7 +844,7 @@ static bool gn_use_fused(int n, int cin, int hw, int groups) {
 
 
 // partial (per-group pairs) + apply-with-fold: two launches where c2d_groupnorm_stats +
-// c2d_groupnorm_apply take three (C2D_GN_FOLD=0 restores those, A/B only).  Needs groups <= 256.
+// c2d_groupnorm_apply take three (C2D_TUNE_GN_FOLD=0 restores those, A/B only).  Needs groups <= 256.
 // Every apply workgroup folds all its image's partial pairs (nblk x groups x 8 B).  Rows per
 // partial block stop at 128, so a 512^2 VAE image has 2048 blocks (512 KB of L2 reads per apply
 // workgroup at 32 groups); measured against the three-launch path (parallel finalize +

@@ -153,26 +153,26 @@ class BasicTransformerBlock(nn.Module):
         self.ff = FeedForward(dim)
         # LayerNorm folded into the GEMM after it (C2D_PRO_LNFOLD, the panel GEMM's K = 320 / 640: the
         # kernel normalises its LDS panel in place): W diag(gamma) and b + W beta for norm1 -> fused
-        # QKV, norm2 -> to_q and norm3 -> GEGLU (finalize); used where _lnf_on says so
+        # QKV, norm2 -> to_q and norm3 -> GEGLU, built by finalize (only with FOLD_LN, so a C2D_LN_FOLD=0
+        # model holds no second copy); used where _lnf_on says so, and only once finalize has run
         self.lnf = dim in (320, 640)
-        inner = self.attn1.heads * self.attn1.dim_head
-        kp = self.attn1.kpad_q
-        for name, rows in (("qkv", 3 * inner), ("q", inner), ("ff", self.ff.net[0].proj.out_features)):
-            self.register_buffer(f"lnf_{name}_w", torch.zeros(rows, kp, dtype=torch.float16) if self.lnf else None,
-                                 persistent=False)
-            self.register_buffer(f"lnf_{name}_b", torch.zeros(rows) if self.lnf else None, persistent=False)
+        self.lnf_folded = False
+        for name in ("qkv", "q", "ff"):
+            self.register_buffer(f"lnf_{name}_w", None, persistent=False)
+            self.register_buffer(f"lnf_{name}_b", None, persistent=False)
 
     @torch.no_grad()
     def finalize(self) -> None:
-        if not self.lnf:
+        if not (self.lnf and FOLD_LN):
             return
         c = self.norm1.c
         wq = torch.cat([self.attn1.to_q.weight, self.attn1.to_k.weight, self.attn1.to_v.weight], 0)
         for name, w, b, norm in (("qkv", wq, None, self.norm1), ("q", self.attn2.to_q.weight, None, self.norm2),
                                  ("ff", self.ff.net[0].proj.weight, self.ff.net[0].proj.bias, self.norm3)):
             wf, bf = ops.fold_layernorm(w, b, norm.weight, norm.bias, c)
-            getattr(self, f"lnf_{name}_w").copy_(wf)
-            getattr(self, f"lnf_{name}_b").copy_(bf)
+            setattr(self, f"lnf_{name}_w", wf.contiguous())
+            setattr(self, f"lnf_{name}_b", bf.contiguous())
+        self.lnf_folded = True
 
     def _lnf_on(self, m: int, cout: int, geglu: bool) -> bool:
         """Fold the LayerNorm into this GEMM: where the planner runs it on the panel kernel anyway,
@@ -180,7 +180,7 @@ class BasicTransformerBlock(nn.Module):
         planner's tile on every UNet shape measured (profiles/r05_ln_fold.txt: to_q 320 -> 320 at
         c3 42.8 -> 34.7 us, c5's fused QKV 105.9 -> 92.4); at K = 640 only the panel shapes gain."""
         c = self.norm1.c
-        return (FOLD_LN and self.lnf and ops.panel_gemm(m, c, cout, geglu, lnfold=True)
+        return (self.lnf_folded and ops.panel_gemm(m, c, cout, geglu, lnfold=True)
                 and (ops.panel_gemm(m, c, cout, geglu) or (c == 320 and m >= 8192)))
 
     def _attend(self, attn: Attention, x, h, ehs, mask, kwargs):
@@ -263,7 +263,10 @@ class Transformer2DModel(nn.Module):
     def finalize(self) -> None:
         """Fold the feed-forward's output Linear into proj_out (both 1x1 maps on the C
         channels, only the block residual between them): Wf = Wp W2 in fp32 from the fp16
-        weights, rounded once; bias Wp b2 + bp."""
+        weights, rounded once; bias Wp b2 + bp.  Also finalizes the block (its LayerNorm folds), so a
+        standalone Transformer2DModel is complete after this call."""
+        for blk in self.transformer_blocks:
+            blk.finalize()
         if not self.fold_ok:
             return
         c = self.proj_out.cout
@@ -468,7 +471,7 @@ class UNet2DConditionModel(nn.Module):
     @torch.no_grad()
     def finalize(self) -> None:
         for m in self.modules():
-            if isinstance(m, (Attention, Transformer2DModel, BasicTransformerBlock)):
+            if isinstance(m, (Attention, Transformer2DModel)):   # Transformer2DModel finalizes its blocks
                 m.finalize()
         rs = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
         self.w_temb_all.copy_(torch.cat([r.time_emb_proj.weight for r in rs], 0))

@@ -125,7 +125,7 @@ int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
  * K slices whose partials cancel -- each far above the output, e.g. beyond the fp16 range
  * while the output fits -- combine to the same result as the single-pass GEMM
  * (tests/test_kernels_gpu.py::test_split_k_cancelling_partials_beyond_fp16).
- * C2D_SPLITK_F16=1 (A/B only, read once per process) stores them rounded to fp16: half the
+ * A variant build with -DC2D_TUNE_SPLITK_F16=1 (A/B only) stores them rounded to fp16: half the
  * slab bytes, but a partial beyond +-65504 becomes inf and cancelling partials lose
  * 2^-11 of their own magnitude.
  */
@@ -145,8 +145,8 @@ int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit);
  * Test / tuning hook: force the LDS-DMA tile configuration (tile_id, one of the ids
  * c2d_conv2d_igemm_plan reports) and the K split (ksplit; 0 = the planner's) of every
  * later eligible c2d_conv2d_igemm call in the process; c2d_set_plan_override(0, 0)
- * restores the planner.  Process-wide (atomic), set explicitly: the library never reads
- * a plan from the environment.  C2D_E_ARG for negative values or ksplit > 64.
+ * restores the planner.  Process-wide (atomic), set explicitly: the library reads no
+ * environment variable at all (its tuning constants are compile-time, csrc/common.h).  C2D_E_ARG for negative values or ksplit > 64.
  */
 int c2d_set_plan_override(int tile_id, int ksplit);
 

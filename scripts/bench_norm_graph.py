@@ -1,5 +1,6 @@
 """Per-shape GroupNorm(+SiLU) cost as the UNet sees it: 20 c2d_groupnorm calls captured
-in one graph and replayed (no Python launch overhead).  C2D_GN_FUSED_HW selects the path."""
+in one graph and replayed (no Python launch overhead).  A variant build (-DC2D_TUNE_GN_FUSED_HW=..., loaded
+through C2D_LIB) selects the path."""
 import os
 import sys
 from pathlib import Path

@@ -3,6 +3,9 @@
 # cancels.  A variant is "label:VAR=val,VAR2=val" (environment for that arm; C2D_LIB=<path> selects
 # another build of libc2d_hip.so, PYROOT=<dir> another Python tree with its own bench.py).
 #   VARIANTS="fold0:C2D_FOLD_FF_OUT=0 fold1:C2D_FOLD_FF_OUT=1" bash scripts/gpu_ab.sh
+# The library reads no environment: a kernel-side candidate is a variant build made here first
+#   python -m clap2diffusion_amd.build --variant gn0 --define C2D_TUNE_GN_FOLD=0
+#   VARIANTS="base:C2D_LIB=clap2diffusion_amd/libc2d_hip.so gn0:C2D_LIB=clap2diffusion_amd/libc2d_hip_gn0.so"
 #   CMD=norm   each arm runs scripts/bench_norm_graph.py (graph-replayed GN / LN shapes)
 #   CMD=shapes each arm runs scripts/unet_shapes.py (per-shape GEMM breakdown)
 #   CMD=bench  (default) the bench line with BENCH_ARGS (default: short, no CPU / PMC / configs)

@@ -1,5 +1,6 @@
 """c5 (N = 8, 96^2) level-0 convs whose one-slice grid is one round + a tail: graph-replayed device time
-per call and output equality vs the torch fp32 reference; run with C2D_TAIL_SPLIT=0 / 1."""
+per call and output equality vs the torch fp32 reference; run against the default library and a variant build
+(build.py --variant notail --define C2D_TUNE_TAIL_SPLIT=0, loaded through C2D_LIB); TAIL names the arm in the output."""
 import math
 import os
 import sys
@@ -63,5 +64,5 @@ for cin, c1, cout, up, res, tmb in ((320, 0, 320, False, True, False), (320, 320
     if r is not None:
         ref = ref + r.permute(0, 3, 1, 2).float()
     err = ((out.permute(0, 3, 1, 2).float() - ref).norm() / ref.norm()).item()
-    print(f"C2D_TAIL_SPLIT={os.environ.get('C2D_TAIL_SPLIT', '1')} 3x3 {cin}+{c1}->{cout} up={int(up)}: "
+    print(f"TAIL={os.environ.get('TAIL', '1')} 3x3 {cin}+{c1}->{cout} up={int(up)}: "
           f"{us:7.1f} us  rel-L2 {err:.2e}", flush=True)

@@ -129,6 +129,9 @@ int main() {
         e = desc(16, 64, 64, 320, 0, 3, 1, 320, C2D_ACT_NONE);   // a 3x3 conv has no whole-row K
         e.pro = C2D_PRO_LNFOLD; e.pro_eps = 1e-5f;        CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
         e = d; e.resid = d.out; e.resid_ld = 960;         CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
+        // a descriptor the DMA kernels do not take at all: the plan query agrees with the run (E_SHAPE)
+        e = d; e.up = 1;                                  CHECK(c2d_conv2d_igemm_plan(&e, &tile, &split) == C2D_E_SHAPE);
+        CHECK(c2d_conv2d_igemm(&e, nullptr) == C2D_E_SHAPE);
     }
     for (int nb : {1, 2, 8})                                            // VAE decoder
         for (int hw : {64, 128, 256, 512})
