@@ -88,14 +88,37 @@ def family_fractions(den):
     unique call timed as a graph of back-to-back replays (scripts/ledger.py, whose full per-shape
     table for c3 / c2 is profiles/r05_ledger_*.txt)."""
     sys.path.insert(0, str(ROOT / "scripts"))
-    from ledger import step_ledger
-    rows, fams, meta = step_ledger(den)
+    from ledger import PEAK_BYTES, PEAK_FLOPS, step_ledger
+    rows, fams, meta = step_ledger(den, situ=True)
     out = {}
     for f, s in fams.items():
         out[f] = round(s["mfma_frac"] if s["flop"] > 0 else s["frac"], 4)
+    step_ms = None if meta["step_us"] is None else meta["step_us"] / 1e3
+
+    def frac_of(flop, byts, us):
+        return round((flop / PEAK_FLOPS if flop > 0 else byts / PEAK_BYTES) * 1e6 / us, 4) if us > 0 else None
+    si = meta["in_situ"]
+    situ_frac = {f: frac_of(fams[f]["flop"], fams[f]["bytes"], us) for f, us in si["family_us"].items()}
+    all_us = si["sequence_us"]
+    situ_frac["all"] = frac_of(fams["all"]["flop"], 0.0, all_us)
+    r, us = max(si["heavy"], key=lambda t: t[1])
+    dom = {"kernel": f"{r['family']}: {r['desc']}", "plan": r["plan"], "calls_per_step": r["calls"],
+           "ms_per_step_in_situ": round(us / 1e3, 3),
+           "share_of_step": None if step_ms is None else round(us / 1e3 / step_ms, 4),
+           "frac_in_situ": frac_of(r["calls"] * r["flop"], r["calls"] * r["bytes"], us),
+           "us_per_call_isolated": round(r["us"], 1)}
     return out, {"ledger_ms_per_step": round(fams["all"]["us"] / 1e3, 3),
-                 "step_graph_ms": None if meta["step_us"] is None else round(meta["step_us"] / 1e3, 3),
+                 "step_graph_ms": None if step_ms is None else round(step_ms, 3),
+                 "ledger_gap_ms": None if step_ms is None else round(step_ms - fams["all"]["us"] / 1e3, 3),
                  "family_ms_per_step": {f: round(s["us"] / 1e3, 3) for f, s in fams.items()},
+                 "family_frac_in_situ": situ_frac,
+                 "family_ms_in_situ": {f: round(u / 1e3, 3) for f, u in si["family_us"].items()},
+                 "sequence_graph_ms": round(all_us / 1e3, 3),
+                 "dominant_by_time": dom,
+                 "in_situ_source": "scripts/ledger.py in_situ: the step's recorded c2d calls captured in order as one graph "
+                                   "(sequence_graph_ms) and again without each family / heavy signature; a family's in-situ "
+                                   "time is the difference, its frac = its FLOP (bytes) / (that time x 2.5 PF/s (8 TB/s)); "
+                                   "all = every FLOP of the step over the sequence time",
                  "family_source": "scripts/ledger.py step_ledger: every c2d call of one denoise step, each unique "
                                   "call timed as a graph of 10 back-to-back replays; FLOP / (t x 2.5 PF/s) for "
                                   "families with FLOP, bytes / (t x 8 TB/s) for norms and elementwise"}

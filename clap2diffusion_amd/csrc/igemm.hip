@@ -795,12 +795,14 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
-C2D_TILE_FN(42); C2D_TILE_FN(70);
+C2D_TILE_FN(42); C2D_TILE_FN(43); C2D_TILE_FN(44); C2D_TILE_FN(70);
 #if C2D_PART(1)
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
 C2D_TILE_FN(50) { (void)ksize; (void)cout; run_pps(p, s); }   // persistent 192x256, carried epilogue (1x1)
-C2D_TILE_FN(42) { (void)ksize; (void)cout; run_pp16r<5>(p, s); }   // 256x320 row-ring 3x3 over a zero-bordered source
+C2D_TILE_FN(42) { (void)ksize; (void)cout; run_pp16r<5>(p, 42, s); }   // 256x320 row-ring 3x3, output width 64
+C2D_TILE_FN(43) { (void)ksize; (void)cout; run_pp16r<5>(p, 43, s); }   // 128x320 row-ring 3x3, output width 32
+C2D_TILE_FN(44) { (void)ksize; (void)cout; run_pp16r<5>(p, 44, s); }   // 128x320 row-ring 3x3, output width 16
 #endif
 #if C2D_PART(2)
 C2D_TILE_FN(25) { run_m32<4, 2, 2, 5, 64, 2, 3, 0, true>(p, ksize, cout, s); }   // 256x320, 8 waves of 64x160
@@ -844,8 +846,11 @@ static const DmaTile kDmaTiles[] = {
     // two workgroups per CU (<= 80 KiB of LDS): the under-filled 1x1 / 3x3 shapes
     {8, 128, 160, 2, 0.0f, false},
     {9, 64, 160, 2, 0.0f, false},
-    // row-ring 3x3 over a zero-bordered source (igemm_pp16r.h): chosen by plan_for only
+    // row-ring 3x3 over a zero-bordered source (igemm_pp16r.h), one per output width (64 / 32 / 16):
+    // chosen by plan_for only
     {42, 256, 320, 1, 0.0f, false},
+    {43, 128, 320, 1, 0.0f, false},
+    {44, 128, 320, 1, 0.0f, false},
 };
 struct DmaPlan { int id, split, nkt; };
 
@@ -990,15 +995,16 @@ static bool plan_hint(int ksize, long M, int kpad, int cout, bool geglu, DmaPlan
     return false;
 }
 
-// tile 42 plan: split-K slices own whole channel blocks (9 K steps each)
-static DmaPlan rr_plan(int nk, int split) {
+// row-ring plan (tiles 42 / 43 / 44): split-K slices own whole channel blocks (9 K steps each)
+static DmaPlan rr_plan(int id, int nk, int split) {
     const int ncb = nk / 9;
     const int sp = split < 1 ? 1 : (split > ncb ? ncb : split);
     const int cbs = (ncb + sp - 1) / sp;
-    return {42, (ncb + cbs - 1) / cbs, 9 * cbs};
+    return {id, (ncb + cbs - 1) / cbs, 9 * cbs};
 }
 
-static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize, bool rr_ok = false,
+// rr_id: the row-ring tile this descriptor can run on (rr_tile), 0 = none
+static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ksize, int rr_id = 0,
                         bool panel_ok = false) {
     const bool geglu = act == C2D_ACT_GEGLU;
     const int nk = kpad / 64;
@@ -1007,14 +1013,24 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
         if (panel_ok && gemm_split() <= 1) return {70, 1, nk};
         id = 0;
     }
-    if (id == 42) {
-        if (rr_ok) return rr_plan(nk, gemm_split());
+    if (id == 42 || id == 43 || id == 44) {
+        if (rr_id == id) return rr_plan(id, nk, gemm_split());
         id = 0;
     }
-    // the row-ring 3x3 (tile 42) on a zero-bordered source once its 256 x 320 tiles fill the chip
-    // (c3's level-0 ResnetBlock2D convs); under-filled grids keep the planner's tiles over the
-    // padded image (a valid 3x3, every tap in bounds)
-    if (!id && rr_ok && !gemm_split() && cout % 320 == 0 && (M / 256) * (cout / 320) >= 192) return rr_plan(nk, 1);
+    // the row-ring 3x3 on a zero-bordered source once its tiles fill the chip: tile 42 (256 x 320,
+    // width 64: c3's level-0 ResnetBlock2D convs), tile 43 (128 x 320, width 32: level 1, 256 tiles
+    // at N = 16 with no split), tile 44 (128 x 320, width 16: level 2, 128 tiles -> 2 K slices);
+    // under-filled grids keep the planner's tiles over the padded image (a valid 3x3, every tap in
+    // bounds).  Graph-replayed per-shape A/B (scripts/rowring_ab.py, profiles/r06_rowring_ab.txt):
+    // tile 43 beats (40, 2) by 5-11 % up to 15 channel blocks (640 +res 125.3 -> 111.6 us) and loses
+    // 2 % at 30 (the 1920 -> 640 up-block conv, whose 270 K steps amortise the split's combine);
+    // tile 44 (2 slices) beats (40, 4) at 10 channel blocks, ties at 20, loses at 40
+    if (!id && rr_id && !gemm_split() && cout % 320 == 0) {
+        const long tiles = (M / (rr_id == 42 ? 256 : 128)) * (cout / 320);
+        const int ncb = nk / 9;
+        if (tiles >= 192 && (rr_id != 43 || ncb < 30)) return rr_plan(rr_id, nk, 1);
+        if (rr_id == 44 && tiles >= 96 && ncb >= 4 && ncb <= 10) return rr_plan(rr_id, nk, 2);
+    }
     if (!id && !gemm_split()) {   // a forced split (tile left to the planner) skips the table
         DmaPlan pl;
         if (plan_hint(ksize, M, kpad, cout, geglu, pl) && (pl.id != 50 || pps_ok) && (pl.id != 70 || panel_ok)) return pl;
@@ -1086,6 +1102,8 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
     p.nkt = pl.nkt;
     switch (pl.id) {
         case 42: return run_tile_42(p, ksize, cout, s);
+        case 43: return run_tile_43(p, ksize, cout, s);
+        case 44: return run_tile_44(p, ksize, cout, s);
         case 25: return run_tile_25(p, ksize, cout, s);
         case 40: return run_tile_40(p, ksize, cout, s);
         case 41: return run_tile_41(p, ksize, cout, s);
@@ -1123,10 +1141,10 @@ static bool panel_eligible(const c2d_conv_desc* d) {
            epi_direct_ok(d) && dma_eligible(d) && (size_t)d->n * d->oh * d->ow * d->out_ld * 2 < (1u << 31);
 }
 
-// the row-ring tile 42 (igemm_pp16r.h) applies to this descriptor
-static bool rr_eligible(const c2d_conv_desc* d) {
-    return d->src_pad && d->pro == C2D_PRO_NONE && pp16r_shape_ok(d->ksize, d->stride, 0, d->c1, d->c0, d->ow, d->oh, d->w + 2) &&
-           d->oh == d->h && d->ow == d->w && d->kpad == 9 * d->c0;
+// the row-ring tile (igemm_pp16r.h: 42 / 43 / 44 by output width) this descriptor can run on, 0 = none
+static int rr_eligible(const c2d_conv_desc* d) {
+    if (!(d->src_pad && d->pro == C2D_PRO_NONE && d->oh == d->h && d->ow == d->w && d->kpad == 9 * d->c0)) return 0;
+    return pp16r_tile_for(d->ksize, d->stride, 0, d->c1, d->c0, d->ow, d->oh, d->w + 2);
 }
 
 // Image split of a quantisation tail.  A one-slice plan whose grid is whole rounds of the chip plus

@@ -158,10 +158,13 @@ def panel_gemm(m: int, k: int, cout: int, geglu: bool, lnfold: bool = False) -> 
     return rc == 0 and tid.value == 70
 
 
+ROWRING_TILES = (42, 43, 44)   # igemm_pp16r.h: output width 64 / 32 / 16
+
+
 @functools.lru_cache(maxsize=None)
 def rowring_conv(n: int, h: int, w: int, cin: int, cout: int) -> bool:
-    """Does c2d's planner run a 3x3 stride-1 conv (n x h x w, cin -> cout) on the row-ring tile 42
-    when its source is zero-bordered?  (Asked of the library, c2d_conv2d_igemm_plan: the padded
+    """Does c2d's planner run a 3x3 stride-1 conv (n x h x w, cin -> cout) on a row-ring tile (42 / 43
+    / 44, by output width) when its source is zero-bordered?  (Asked of the library, c2d_conv2d_igemm_plan: the padded
     layout is worth writing only where that kernel reads it.)"""
     import ctypes
     from ._lib import ConvDesc, check, lib
@@ -171,7 +174,7 @@ def rowring_conv(n: int, h: int, w: int, cin: int, cout: int) -> bool:
     d.out_ld = cout
     tid, ks = ctypes.c_int(), ctypes.c_int()
     check(lib().c2d_conv2d_igemm_plan(ctypes.byref(d), ctypes.byref(tid), ctypes.byref(ks)), "c2d_conv2d_igemm_plan")
-    return tid.value == 42
+    return tid.value in ROWRING_TILES
 
 
 def conv_workspace_bytes(n: int, h: int, w: int, c0: int, c1: int, cout: int, ksize: int) -> int:

@@ -158,8 +158,47 @@ def _time_graph(fn, reps: int, tries: int = 3) -> float:
     return best
 
 
-def call_ledger(run, reps: int = 10):
-    """Ledger of the c2d calls one invocation of run() issues; -> (rows, families, n_calls)."""
+def _call_kwargs(b, out) -> dict:
+    kw = dict(b.arguments)
+    if "out" in kw and kw["out"] is None and torch.is_tensor(out):
+        kw["out"] = out
+    return kw
+
+
+def in_situ(rec, rows, top: int = 3, tries: int = 3):
+    """In-situ times of the families and of the `top` heaviest signatures of a recorded call
+    sequence: the whole sequence (every recorded call, in its recorded order, on its recorded
+    tensors) is captured as ONE graph and timed, then once more per family / signature with that
+    family's / signature's calls left out; a family's in-situ time is the difference.  Unlike the
+    10x back-to-back replays of the rows (each call's weights hot in L2 / MALL, the clock of a
+    repeated kernel), every call here runs after its real predecessor, as in the step.
+    -> (sequence us, {family: us}, [(row, us)])"""
+    calls = []
+    for name, b, out in rec.calls:
+        fam = _work(name, b.arguments, out)[0]
+        calls.append((rec.orig[name], _call_kwargs(b, out), fam, (name, _sig(dict(b.arguments)))))
+
+    def seq_us(skip) -> float:
+        kept = [(fn, kw) for fn, kw, fam, sg in calls if not skip(fam, sg)]
+
+        def run():
+            for fn, kw in kept:
+                fn(**kw)
+        return _time_graph(run, 1, tries)
+
+    with torch.no_grad():
+        whole = seq_us(lambda fam, sg: False)
+        fam_us = {}
+        for fam in dict.fromkeys(c[2] for c in calls):
+            fam_us[fam] = whole - seq_us(lambda f, sg, fam=fam: f == fam)
+        heavy = sorted(rows, key=lambda r: -r["calls"] * r["us"])[:top]
+        sig_us = [(r, whole - seq_us(lambda f, sg, key=r["key"]: sg == key)) for r in heavy]
+    return whole, fam_us, sig_us
+
+
+def call_ledger(run, reps: int = 10, keep_recording: bool = False):
+    """Ledger of the c2d calls one invocation of run() issues; -> (rows, families, n_calls)
+    (keep_recording: and the Recorder, for in_situ)."""
     rec = Recorder()
     with torch.no_grad(), rec:
         run()
@@ -169,11 +208,10 @@ def call_ledger(run, reps: int = 10):
         groups.setdefault((name, _sig(dict(b.arguments))), []).append((b, out))
     rows = []
     with torch.no_grad():
-        for (name, _), lst in groups.items():
+        for key, lst in groups.items():
+            name = key[0]
             b, out = lst[0]
-            kw = dict(b.arguments)
-            if "out" in kw and kw["out"] is None and torch.is_tensor(out):
-                kw["out"] = out
+            kw = _call_kwargs(b, out)
             fn = rec.orig[name]
             plan = None
             if name == "conv":
@@ -184,7 +222,7 @@ def call_ledger(run, reps: int = 10):
             fam, desc, flop, byts = _work(name, b.arguments, out)
             roof_us = max(flop / PEAK_FLOPS, byts / PEAK_BYTES) * 1e6
             bound = "mfma" if flop / PEAK_FLOPS >= byts / PEAK_BYTES else "hbm"
-            rows.append(dict(op=name, family=fam, desc=desc, calls=len(lst), plan=plan, us=us, flop=flop,
+            rows.append(dict(op=name, key=key, family=fam, desc=desc, calls=len(lst), plan=plan, us=us, flop=flop,
                              bytes=byts, roof_us=roof_us, bound=bound, frac=roof_us / us,
                              lost_us=len(lst) * (us - roof_us)))
     rows.sort(key=lambda r: -r["lost_us"])
@@ -202,15 +240,22 @@ def call_ledger(run, reps: int = 10):
     for s_ in fams.values():
         s_["frac"] = s_["roof_us"] / s_["us"] if s_["us"] else 0.0
         s_["mfma_frac"] = s_["flop"] / (s_["us"] * 1e-6) / PEAK_FLOPS if s_["us"] else 0.0
+    if keep_recording:
+        return rows, fams, len(rec.calls), rec
     return rows, fams, len(rec.calls)
 
 
-def step_ledger(den, reps: int = 10):
+def step_ledger(den, reps: int = 10, situ: bool = False):
     """Ledger of one step of a GraphDenoiser `den` (its eager body); -> (rows, families, meta).
-    rows: dicts sorted by lost us per step.  The denoiser's step counter is restored."""
+    rows: dicts sorted by lost us per step.  The denoiser's step counter is restored.
+    situ: also the in-situ family / heaviest-signature times (in_situ) in meta["in_situ"]."""
     idx0 = den.step_idx.clone()
     den.step_idx.zero_()
-    rows, fams, ncalls = call_ledger(den._body, reps)
+    rows, fams, ncalls, rec = call_ledger(den._body, reps, keep_recording=True)
+    situ_meta = None
+    if situ:
+        whole, fam_us, sig_us = in_situ(rec, rows)
+        situ_meta = dict(sequence_us=whole, family_us=fam_us, heavy=sig_us)
     step_us = None
     if den.graph is not None:
         ts = []
@@ -224,7 +269,8 @@ def step_ledger(den, reps: int = 10):
             ts.append(e0.elapsed_time(e1) * 1e3)
         step_us = min(ts)
     den.step_idx.copy_(idx0)
-    meta = dict(n_calls=ncalls, unique=len(rows), step_us=step_us, n=2 * den.b, res=den.h, what="denoise step")
+    meta = dict(n_calls=ncalls, unique=len(rows), step_us=step_us, n=2 * den.b, res=den.h, what="denoise step",
+                in_situ=situ_meta)
     return rows, fams, meta
 
 
@@ -253,6 +299,20 @@ def format_ledger(rows, fams, meta) -> str:
     for f, s in sorted(fams.items(), key=lambda kv: -kv[1]["us"]):
         L.append(f"{f:12s} {s['calls']:5d} {s['us'] / 1e3:8.3f} {100 * s['us'] / tot:5.1f}% {s['flop'] / 1e9:9.1f} "
                  f"{s['bytes'] / 1e6:9.1f} {s['roof_us'] / 1e3:8.3f} {s['frac']:6.3f} {s['mfma_frac']:6.3f}")
+    si = meta.get("in_situ")
+    if si:
+        L += ["", f"# in situ (the recorded call sequence as one graph, {si['sequence_us'] / 1e3:.3f} ms; a family's "
+                  "time = sequence - sequence without it)",
+              f"{'family':12s} {'ms/step':>8s} {'share':>6s} {'frac':>6s}"]
+        for f, us in sorted(si["family_us"].items(), key=lambda kv: -kv[1]):
+            s_ = fams[f]
+            work = s_["flop"] / PEAK_FLOPS if s_["flop"] > 0 else s_["bytes"] / PEAK_BYTES
+            L.append(f"{f:12s} {us / 1e3:8.3f} {100 * us / si['sequence_us']:5.1f}% {work * 1e6 / us if us > 0 else 0:6.3f}")
+        for r, us in si["heavy"]:
+            work = r["flop"] / PEAK_FLOPS if r["flop"] > 0 else r["bytes"] / PEAK_BYTES
+            L.append(f"  heavy: {r['family']}: {r['desc']} x{r['calls']}: {us / 1e3:.3f} ms in situ "
+                     f"({us / r['calls']:.1f} us/call, frac {r['calls'] * work * 1e6 / us if us > 0 else 0:.3f}; "
+                     f"isolated {r['us']:.1f} us/call)")
     L += ["", f"{'lost us':>8s} {'calls':>5s} {'us/call':>8s} {'roof us':>8s} {'bound':>5s} {'frac':>6s} "
               f"{'GFLOP':>8s} {'MB':>8s} {'plan':>8s}  family / shape"]
     for r in rows:
@@ -307,7 +367,7 @@ def main():
     with torch.no_grad():
         den.run(torch.randn(B, 4, a.res, a.res, generator=g).to(dev))   # packs weights, captures the step graph
     torch.cuda.synchronize()
-    rows, fams, meta = step_ledger(den, a.reps)
+    rows, fams, meta = step_ledger(den, a.reps, situ=True)
     txt = format_ledger(rows, fams, meta)
     print(txt, flush=True)
     if a.out:

@@ -20,7 +20,7 @@ static int fails = 0;
         }                                                                     \
     } while (0)
 
-static const int kTiles[] = {0, 1, 2, 3, 7, 8, 9, 25, 28, 29, 40, 41, 42, 50, 60, 61, 62, 70};
+static const int kTiles[] = {0, 1, 2, 3, 7, 8, 9, 25, 28, 29, 40, 41, 42, 43, 44, 50, 70};
 
 static c2d_conv_desc desc(int n, int h, int w, int c0, int c1, int ksize, int stride, int cout, int act) {
     static char dummy[64] __attribute__((aligned(16)));
@@ -86,17 +86,26 @@ int main() {
         }
     check_plan(desc(16, 64, 64, 640, 320, 3, 1, 320, C2D_ACT_NONE));   // up-block skip concat
     check_plan(desc(16, 64, 64, 320, 0, 3, 2, 320, C2D_ACT_NONE));     // stride-2 downsample
-    // zero-bordered sources (c2d_groupnorm_pad): the row-ring tile 42 at c3's level 0, planner tiles elsewhere
+    // zero-bordered sources (c2d_groupnorm_pad): the row-ring tiles at c3's levels 0 / 1 / 2 (42 / 43 /
+    // 44 by width; 43 up to 29 channel blocks, 44 with 2 slices up to 10), planner tiles elsewhere
     for (int nb : {2, 16})
         for (int hw : {64, 32, 16})
-            for (int cc : {320, 640, 960}) {
-                c2d_conv_desc d = desc(nb, hw, hw, cc, 0, 3, 1, 320, C2D_ACT_NONE);
-                d.src_pad = 1;
-                check_plan(d);
-                int tile = -1, split = -1;
-                CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK);
-                CHECK((tile == 42) == (nb == 16 && hw == 64));
-            }
+            for (int cc : {320, 640, 960, 1280, 1920})
+                for (int co : {320, 640, 1280}) {
+                    c2d_conv_desc d = desc(nb, hw, hw, cc, 0, 3, 1, co, C2D_ACT_NONE);
+                    d.src_pad = 1;
+                    check_plan(d);
+                    int tile = -1, split = -1;
+                    CHECK(c2d_conv2d_igemm_plan(&d, &tile, &split) == C2D_OK);
+                    const long m = (long)nb * hw * hw;
+                    const int ncb = cc / 64;
+                    const bool r42 = hw == 64 && (m / 256) * (co / 320) >= 192;
+                    const bool r43 = hw == 32 && (m / 128) * (co / 320) >= 192 && ncb < 30;
+                    const bool r44 = hw == 16 && (m / 128) * (co / 320) >= 96 && ncb >= 4 && ncb <= 10;
+                    CHECK((tile == 42) == r42);
+                    CHECK((tile == 43) == r43);
+                    CHECK((tile == 44) == r44);   // (split 2 only with a workspace; none here)
+                }
     {
         c2d_conv_desc d = desc(16, 64, 64, 320, 0, 3, 2, 320, C2D_ACT_NONE);
         d.src_pad = 1;   // a padded source is stride 1 only

@@ -251,11 +251,19 @@ def test_groupnorm_pad(dev, n, h, w, c0, c1, silu):
     (2, 32, 320, 640, 0, 0, "resid"),     # other tiles over the padded source (a valid 3x3)
     (2, 16, 1280, 1280, 0, 0, "temb"),
     (3, 8, 640, 320, 7, 2, "plain"),
+    (16, 32, 640, 640, 0, 0, "resid"),    # c3's level-1 conv2: the planner's tile 43 (width 32), no split
+    (16, 32, 960, 640, 0, 0, "temb"),     # a level-1 up block's conv1 over the padded concat (15 channel blocks)
+    (16, 16, 640, 1280, 0, 0, "temb"),    # c3's level-2 first conv1: tile 44 (width 16), 2 K slices
+    (2, 32, 320, 640, 43, 1, "plain"),    # forced tile 43 on a small grid
+    (2, 32, 640, 320, 43, 3, "temb"),     # forced split: 10 channel blocks in 3 slices (4, 4, 2)
+    (1, 16, 960, 320, 44, 1, "resid"),    # forced tile 44, one image (two 8-row tiles)
+    (2, 16, 640, 640, 44, 4, "plain"),    # tile 44 with 4 slices of whole channel blocks
 ])
 def test_conv3x3_padded_source(dev, force_plan, n, h, cin, cout, tile, split, form):
-    """3x3 conv over a zero-bordered source (c2d_conv_desc::src_pad): the row-ring tile 42
-    (igemm_pp16r.h: 6 padded image rows staged once per channel block, taps as row-shifted
-    fragment reads) and every other tile as a valid 3x3 over the padded image."""
+    """3x3 conv over a zero-bordered source (c2d_conv_desc::src_pad): the row-ring tiles 42 / 43 / 44
+    (igemm_pp16r.h: the padded image rows of a channel block staged once into a ring of LDS row
+    slots, taps as row-shifted fragment reads; output width 64 / 32 / 16) and every other tile as a
+    valid 3x3 over the padded image."""
     x = gen(n, cin, h, h, seed=151)
     w = gen(cout, cin, 3, 3, seed=152, scale=1.0 / math.sqrt(9 * cin))
     b = gen(cout, seed=153)
@@ -277,14 +285,19 @@ def test_conv3x3_padded_source(dev, force_plan, n, h, cin, cout, tile, split, fo
                        temb=None if temb is None else temb.half().to(dev),
                        resid=None if resid is None else nhwc(resid).half().to(dev))
     assert out.shape == (n, h, h, cout)
+    rr = {64: 42, 32: 43, 16: 44}
     if tile:
         assert plans == [(tile, split)], plans
-    elif n == 16 and h == 64:
-        assert plans[0][0] == 42, plans
+    elif n == 16 and h in rr:
+        assert plans[0][0] == rr[h], plans
     else:
-        assert plans[0][0] != 42, plans
+        assert plans[0][0] not in rr.values(), plans
     if not tile:
-        assert ops.rowring_conv(n, h, h, cin, cout) == (n == 16 and h == 64)
+        assert ops.rowring_conv(n, h, h, cin, cout) == (n == 16 and h in rr)
+    if not tile and n == 16:   # the planner keeps the split 256-row tile where the row ring loses
+        long_k = {32: 1920, 16: 1280}.get(h)
+        if long_k:
+            assert not ops.rowring_conv(n, h, h, long_k, cout)
     close(nchw(out), ref)
 
 

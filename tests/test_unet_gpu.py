@@ -125,8 +125,9 @@ def test_unet_step_c3_batch_matches_oracle(dev, unet_pair):
                     cross_attention_kwargs=mgr.get_audio_kwargs({k: v.to(dev) for k, v in audio.items()})).sample
     torch.cuda.synchronize()
     tiles = {t for t, _ in plans}
-    # 42: the row-ring 3x3 over the zero-bordered GroupNorm output (level-0 ResnetBlock2D convs)
-    assert 25 in tiles and 42 in tiles and any(ks > 1 for _, ks in plans), (tiles, plans[:8])
+    # 42 / 43 / 44: the row-ring 3x3 over the zero-bordered GroupNorm output (level-0 / 1 / 2
+    # ResnetBlock2D convs)
+    assert 25 in tiles and {42, 43, 44} <= tiles and any(ks > 1 for _, ks in plans), (tiles, plans[:8])
     with torch.no_grad():
         e_ref = ref(x, 981, ehs, audio)
     err = rel_l2(e_hip, e_ref)
