@@ -20,11 +20,17 @@ namespace c2d {
 #define ATTN_WPE 4
 #endif
 
+#ifndef C2D_TUNE_ATTN80
+#define C2D_TUNE_ATTN80 1   // d = 80: 1 = the PV row-sum column (round 6), 0 = VALU row sums (round 5; A/B builds)
+#endif
+
 template <int D> struct AttnCfg {
     // K dim of QK^T: full 32-deep chunks on 16x16x32 MFMAs plus, when the rest is
     // exactly 16 deep (d = 80), one 16x16x16 MFMA into a separate accumulator
-    // (added with VALU: no mixed-shape MFMA accumulation chain) instead of a
-    // zero-padded 32 chunk
+    // (added with VALU) instead of a zero-padded 32 chunk.  Round 6 chained it into the
+    // 32-deep accumulators instead (same C/D layout; 3 % faster at L1): the resident-K/V
+    // 64-key case (test_attention[3-8-300-64-80]) came out wrong (rel-L2 0.14), so no
+    // mixed-shape MFMA accumulation chain
     // d < 64 and not a multiple of 32 (d = 40): the whole QK^T on 16x16x16 MFMAs
     // over 16-deep chunks (K = 48 instead of a zero-padded 64)
     static constexpr bool C16 = false;   // measured slower on gfx950: 16x16x16 issues at the 16x16x32 cycle count
@@ -33,7 +39,9 @@ template <int D> struct AttnCfg {
     static constexpr bool TAIL = !C16 && (D % 32) == 16;
     static constexpr int DP = C16 ? NC16 * 16 : TAIL ? NDC * 32 + 16 : (D + 31) / 32 * 32;
     static constexpr int NDC_FULL = C16 ? 0 : TAIL ? NDC : DP / 32;  // 32-deep chunks actually issued
-    static constexpr int DV = (D + 15) / 16 * 16;      // N dim of PV, multiple of 16
+    // N dim of PV, multiple of 16.  d = 80: one more 16-column tile (96) so the PV MFMAs also carry the
+    // row sum (SUM_MFMA): 4 more MFMAs per wave-tile against 32 VALU adds of the per-lane sums
+    static constexpr int DV = (D == 80 && C2D_TUNE_ATTN80) ? 96 : (D + 15) / 16 * 16;
     static constexpr int NDT = DV / 16;
     // K rows: 128-B rows with the 16-B chunk XOR swizzle (chunk ^ ((row >> 1) & 7)) when
     // DP = 64 (conflict-free QK^T fragment reads, PMC-verified need: the padded

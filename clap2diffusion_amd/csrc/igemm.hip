@@ -995,6 +995,40 @@ static bool plan_hint(int ksize, long M, int kpad, int cout, bool geglu, DmaPlan
     return false;
 }
 
+// Measured row-ring plans (tile, split) for zero-bordered-source 3x3 shapes where the rules below
+// lose >= 3 % to one (scripts/rr_sweep.py: the production route on the unpadded source against the
+// row-ring tile with every split of whole channel blocks, graph-replayed, profiles/r06_rr_sweep_*.txt).
+// Keyed on (M = N * H * W, kpad, cout); only consulted when the descriptor's width has a row-ring tile.
+struct RrHint { long M; int kpad, cout, id, split; };
+static const RrHint kRrHints[] = {
+    // N = 2 (c1 / c2; profiles/r06_rr_sweep_b1.txt): every ResnetBlock2D 3x3 of levels 0-2 except the
+    // level-0 320 -> 320 (tied with (7, 4) on the unpadded source)
+    {8192, 5760, 320, 42, 5},   // N = 2 64^2 640 -> 320: 56.7 -> 51.9 us
+    {8192, 8640, 320, 42, 8},   // N = 2 64^2 960 -> 320: 71.2 -> 63.1 us
+    {2048, 2880, 640, 43, 5},   // N = 2 32^2 320 -> 640: 34.5 -> 26.2 us
+    {2048, 5760, 640, 43, 5},   // N = 2 32^2 640 -> 640: 40.1 -> 33.6 us
+    {2048, 8640, 640, 43, 8},   // N = 2 32^2 960 -> 640: 49.3 -> 39.7 us
+    {2048, 11520, 640, 43, 5},   // N = 2 32^2 1280 -> 640: 59.8 -> 49.3 us
+    {2048, 17280, 640, 43, 8},   // N = 2 32^2 1920 -> 640: 73.6 -> 58.6 us
+    {512, 5760, 1280, 44, 10},   // N = 2 16^2 640 -> 1280: 34.7 -> 27.8 us
+    {512, 11520, 1280, 44, 10},   // N = 2 16^2 1280 -> 1280: 44.2 -> 36.2 us
+    {512, 17280, 1280, 44, 15},   // N = 2 16^2 1920 -> 1280: 50.1 -> 45.3 us
+    {512, 23040, 1280, 44, 10},   // N = 2 16^2 2560 -> 1280: 59.8 -> 53.6 us
+};
+
+// a row-ring tile of the same geometry as rr_id (one tile per width today)
+static bool rr_compatible(int id, int rr_id) { return id == rr_id; }
+
+static bool rr_hint(long M, int kpad, int cout, int rr_id, int& id, int& split) {
+    for (const RrHint& h : kRrHints)
+        if (h.M == M && h.kpad == kpad && h.cout == cout && rr_compatible(h.id, rr_id)) {
+            id = h.id;
+            split = h.split;
+            return true;
+        }
+    return false;
+}
+
 // row-ring plan (tiles 42 / 43 / 44): split-K slices own whole channel blocks (9 K steps each)
 static DmaPlan rr_plan(int id, int nk, int split) {
     const int ncb = nk / 9;
@@ -1014,7 +1048,7 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
         id = 0;
     }
     if (id == 42 || id == 43 || id == 44) {
-        if (rr_id == id) return rr_plan(id, nk, gemm_split());
+        if (rr_id && rr_compatible(id, rr_id)) return rr_plan(id, nk, gemm_split());
         id = 0;
     }
     // the row-ring 3x3 on a zero-bordered source once its tiles fill the chip: tile 42 (256 x 320,
@@ -1025,6 +1059,10 @@ static DmaPlan plan_for(long M, int cout, int kpad, int act, bool pps_ok, int ks
     // tile 43 beats (40, 2) by 5-11 % up to 15 channel blocks (640 +res 125.3 -> 111.6 us) and loses
     // 2 % at 30 (the 1920 -> 640 up-block conv, whose 270 K steps amortise the split's combine);
     // tile 44 (2 slices) beats (40, 4) at 10 channel blocks, ties at 20, loses at 40
+    if (!id && rr_id && !gemm_split()) {
+        int hid = 0, sp = 0;
+        if (rr_hint(M, kpad, cout, rr_id, hid, sp)) return rr_plan(hid, nk, sp);
+    }
     if (!id && rr_id && !gemm_split() && cout % 320 == 0) {
         const long tiles = (M / (rr_id == 42 ? 256 : 128)) * (cout / 320);
         const int ncb = nk / 9;

@@ -60,13 +60,27 @@ template <> struct RrSched<10> {   // NS = 16: (c,8),(c,9),(c+1,0),(c+1,1) | (c+
     }
 };
 
-template <int W, int TMW> struct RrGeo {
-    static constexpr int BM = 2 * TMW * 16, R = BM / W, RB = R + 2;
+#ifndef C2D_PP16R_RRSWZ
+#define C2D_PP16R_RRSWZ 0   // 1: tile 42 with round 4's layout (80-row slots, rr_swz; A/B builds)
+#endif
+// Round 4's bank swizzle of tile 42 (A/B builds only): conflict-free for row shifts 0..2 only,
+// repeating every 16 rows, so slots were 80 rows apart.  f = {0,0,1,1,2,2,4,4, 5,5,6,6,2,2,6,6}
+__host__ __device__ constexpr int rr_swz(int r) {
+    constexpr unsigned long long F = 0ull | (0ull << 3) | (1ull << 6) | (1ull << 9) | (2ull << 12) | (2ull << 15) |
+                                     (4ull << 18) | (4ull << 21) | (5ull << 24) | (5ull << 27) | (6ull << 30) |
+                                     (6ull << 33) | (2ull << 36) | (2ull << 39) | (6ull << 42) | (6ull << 45);
+    return (int)((F >> (3 * r)) & 7ull);
+}
+
+template <int W, int BM_> struct RrGeo {
+    static constexpr int BM = BM_, R = BM / W, RB = R + 2;
     static constexpr int PPR = (W + 2 + 7) / 8;                 // pieces per padded row
     // LDS rows per slot: 8 PPR, or 20 at W = 16 (18 pixels: the slot ring of 16 fits beside a 3-slot
     // weight ring).  There the last piece of a row loads its 2 pixels with lanes 0-15 only (LASTL),
     // and slots start at rows = 4 mod 8 on odd slots, whose chunk swizzle is then (r + 4) & 6 (PAR)
-    static constexpr int SP = W == 16 ? 20 : PPR * 8;
+    static constexpr bool RR = C2D_PP16R_RRSWZ && W == 64;
+    static constexpr int SP = RR ? 80 : W == 16 ? 20 : PPR * 8;
+    __host__ __device__ static constexpr int swz(int r) { return RR ? rr_swz(r & 15) : (r & 6); }
     static constexpr bool PAR = (SP % 8) != 0;
     static constexpr int LASTL = SP < PPR * 8 ? ((W + 2) - 8 * (PPR - 1)) * 8 : 64;
     static_assert(SP % 4 == 0 && SP >= W + 2, "slot pitch");
@@ -83,28 +97,38 @@ template <int W, int TMW> struct RrGeo {
 // 3 (tile 43): the pieces of step kt + 2, dealt over both phases and waited one step later
 // (vmcnt(NBP): everything older than this step's weight pieces), so no phase's load section
 // carries all NBP pieces of a step (the 2-phase form dealt them all in phase 0)
-template <int TN, int PH, int W, int TMW, int NB = 2>
+// NRG: row groups of the 8 waves (2: 2 x 4 column waves, the ping-pong layout of igemm_pp16.h;
+// 4: 4 x 2).  Waves 0-3 and 4-7 are the two stagger groups either way (one wave of each per SIMD),
+// group 1 one barrier behind group 0.  A 128 x 160 width-16 tile on the 4 x 2 layout (TMW = 2,
+// 10-MFMA phases; round 6, built and measured: profiles/r06_rr_sweep45_b*.txt) ran c3's level-2
+// 1280 -> 1280 conv unsplit at 175.5 us against 126.8 for (40, 4) and lost at every split: only
+// NRG = 2 is instantiated.
+template <int TN, int PH, int W, int TMW, int NB = 2, int NRG = 2>
 __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
-    typedef RrGeo<W, TMW> G;
+    constexpr int NCW = 8 / NRG;                    // column waves
+    typedef RrGeo<W, NRG * TMW * 16> G;
     typedef typename G::S S;
     static_assert(PH == 2 || PH == 4, "pp16r phases per K step");
     static_assert(NB == 2 || (NB == 3 && PH == 2), "weight ring depth");
-    static_assert(TMW == 8 || (TMW == 4 && PH == 2), "row halves per phase");
+    static_assert(TMW == 8 || (TMW <= 4 && PH == 2), "row halves per phase");
+    static_assert(NRG == 2 || NRG == 4, "row groups");
     constexpr int BK = 64, NW = 8;
     constexpr int RT = PH == 4 ? 4 : TMW;           // 16-row tiles per phase
-    constexpr int BM = G::BM, BN = 4 * TN * 16;
+    constexpr int BM = G::BM, BN = NCW * TN * 16;
     constexpr int RB = 2 * BK;                    // bytes per LDS row
     constexpr int SBYTES = G::SP * RB;            // bytes per row slot
     constexpr int A_BYTES = G::A_BYTES;
     constexpr int BSTAGE = BN * RB;
-    constexpr int NBP = BN / 8 / NW;              // weight pieces per wave per K step
+    constexpr int NPB = BN / 8;                   // weight pieces per K step
+    constexpr int NBP = (NPB + NW - 1) / NW;      // ... per wave (the first NPB % NW waves one more)
     constexpr int PPR = G::PPR, NS = G::NS, ROWB = G::RB;
-    static_assert(NBP * 8 * NW == BN, "weight rows must split evenly over the waves");
+    static_assert(BN % 8 == 0, "whole weight pieces");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wave >> 2, wc = wave & 3;
+    const int wr = wave / NCW, wc = wave - (wave / NCW) * NCW, sg = wave >> 2;
+    const int nbp = (NPB - wave + NW - 1) / NW;   // this wave's weight pieces per K step
     const int l15 = lane & 15, lg = lane >> 4;
     const int lrow = lane >> 3, lchunk = lane & 7;
     const int bid = xcd_remap(blockIdx.x, p.gx * p.gy * p.ksplit);
@@ -127,8 +151,10 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
 
     // A piece lane offset: pixel lrow of the piece, logical chunk lchunk ^ (lrow & 6) (pieces start
     // at LDS rows that are multiples of 8, so the slot swizzle is the same for every piece)
-    const unsigned a_lo0 = (unsigned)(2 * (lrow * cin + ((lchunk ^ (lrow & 6)) << 3)));
-    const unsigned a_lo1 = G::PAR ? (unsigned)(2 * (lrow * cin + ((lchunk ^ ((lrow + 4) & 6)) << 3))) : a_lo0;
+    // (RR: rows 8 k + lrow repeat every 16, so the piece's parity picks the half)
+    const unsigned a_lo0 = (unsigned)(2 * (lrow * cin + ((lchunk ^ G::swz(lrow)) << 3)));
+    const unsigned a_lo1 = (G::PAR || G::RR) ? (unsigned)(2 * (lrow * cin + ((lchunk ^ G::swz(lrow + (G::RR ? 8 : 4))) << 3)))
+                                             : a_lo0;
     // weight rows of this wave's pieces (the M32Loader B addressing)
     unsigned b_off[NBP];
 #pragma unroll
@@ -143,7 +169,7 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
     auto a_piece = [&](int cr, int j, int k) __attribute__((always_inline)) {
         const int s = (int)((unsigned)(ROWB * cr + j) % (unsigned)NS);
         const unsigned soff = a_img + (unsigned)j * a_rowb + 2u * (unsigned)(8 * k * cin + cr * BK);
-        const unsigned lo = (G::PAR && (s & 1)) ? a_lo1 : a_lo0;
+        const unsigned lo = ((G::PAR && (s & 1)) || (G::RR && (k & 1))) ? a_lo1 : a_lo0;
         if (G::LASTL < 64 && k == PPR - 1) {
             if (lane < G::LASTL)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lptr_t)(smem + s * SBYTES + k * 1024), 16, lo, (int)soff, 0, 0);
@@ -151,8 +177,9 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lptr_t)(smem + s * SBYTES + k * 1024), 16, lo, (int)soff, 0, 0);
         }
     };
-    // weight piece i of K step (cr, tap) into ring slot bs
+    // weight piece i of K step (cr, tap) into ring slot bs (i < nbp)
     auto b_piece = [&](int cr, int tap, int bs, int i) __attribute__((always_inline)) {
+        if (NPB % NW != 0 && i >= nbp) return;
         const int k0 = tap * cin + (cb0 + cr) * BK;
         const __amdgpu_buffer_rsrc_t rb = make_rsrc(u_wt + 2 * k0, wbytes - 2 * k0);
         dma_piece(rb, smem + A_BYTES + bs * BSTAGE + (wave + i * NW) * 1024, b_off[i]);
@@ -185,7 +212,7 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
     }
     wait_vm_c<0>();
     C2D_BAR();
-    if (wr) C2D_BAR();   // group 1 runs one barrier behind group 0
+    if (sg) C2D_BAR();   // group 1 runs one barrier behind group 0
 
     f16x8 fa[RT], fb[TN];
     const int nsteps = 9 * ncb;
@@ -202,8 +229,8 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
         const char* SB = smem + A_BYTES + bs * BSTAGE + wc * TN * 16 * RB;
         // A fragment rows: LDS row kx + l15 (+ x0) of the slot of image row ir + ky of block cr
         const int ar = l15 + kx;
-        const int alane = ar * RB + (((lg) ^ (ar & 6)) << 4);   // k32 half 0; half 1: chunk bit 2 flipped
-        const int alane1 = G::PAR ? ar * RB + (((lg) ^ ((ar + 4) & 6)) << 4) : alane;   // odd slots (PAR)
+        const int alane = ar * RB + (((lg) ^ G::swz(ar)) << 4);   // k32 half 0; half 1: chunk bit 2 flipped
+        const int alane1 = G::PAR ? ar * RB + (((lg) ^ G::swz(ar + 4)) << 4) : alane;   // odd slots (PAR)
         const int sbase = ROWB * cr + ky;
 #pragma unroll
         for (int qq = 0; qq < PH; ++qq) {
@@ -246,8 +273,12 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
             }
             if (NB == 2 && qq == (PH == 4 ? 2 : 0) && !C2D_ABL(p.abl, 1)) sched_piece(cr, ky, 3 * wave + kx, more);
             if (qq == PH - 1 && nxt) {   // own pieces the next step reads landed
-                if (NB == 3 && bdeal) wait_vm_c<NBP>();   // (all but this step's weight pieces)
-                else wait_vm_c<0>();
+                if (NB == 3 && bdeal) {   // (all but this step's weight pieces)
+                    if (NPB % NW == 0 || nbp == NBP) wait_vm_c<NBP>();
+                    else wait_vm_c<(NBP > 0 ? NBP - 1 : 0)>();
+                } else {
+                    wait_vm_c<0>();
+                }
             }
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
             C2D_BAR();
@@ -270,7 +301,7 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
         }
         bs = NB == 2 ? (bs ^ 1) : (bs == 2 ? 0 : bs + 1);
     }
-    if (!wr) C2D_BAR();   // balance the stagger
+    if (!sg) C2D_BAR();   // balance the stagger
 #undef C2D_BAR
 
     const int mw0 = m0 + wr * TMW * 16, nw0 = n0 + wc * TN * 16;
@@ -317,7 +348,7 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
         const int wr0 = wr * 32, wc0 = wc * TN * 16;
         static_for<0, TMW / 2>([&](auto pass) __attribute__((always_inline)) {
             constexpr int b0 = 2 * decltype(pass)::value;
-            epi_pass<64, BN, true, 512, TMW * 16>(p, img, PITCHB, m0 + b0 * 16, n0, tid, [&]() __attribute__((always_inline)) {
+            epi_pass<NRG * 32, BN, true, 512, TMW * 16>(p, img, PITCHB, m0 + b0 * 16, n0, tid, [&]() __attribute__((always_inline)) {
                 f32x4 bv[TN];
 #pragma unroll
                 for (int a = 0; a < TN; ++a) bv[a] = bias4(p, nw0 + a * 16 + 4 * lg);
@@ -332,18 +363,19 @@ __global__ void __launch_bounds__(512) igemm_pp16r_kernel(IgemmParams p) {
     }
 }
 
-// LDS of a row-ring tile: the row slots + the 2-slot weight ring, or the epilogue images
-template <int TN, int W, int TMW, int NB>
+// LDS of a row-ring tile: the row slots + the weight ring, or the epilogue images
+template <int TN, int W, int TMW, int NB, int NRG>
 constexpr int pp16r_smem() {
-    constexpr int ring = RrGeo<W, TMW>::A_BYTES + NB * (4 * TN * 16) * 128;
-    constexpr int epi_wg = 64 * (4 * TN * 16 + 4) * 4, epi_wv = 8 * 32 * (TN * 16 + 4) * 4;
+    constexpr int BN = (8 / NRG) * TN * 16;
+    constexpr int ring = RrGeo<W, NRG * TMW * 16>::A_BYTES + NB * BN * 128;
+    constexpr int epi_wg = NRG * 32 * (BN + 4) * 4, epi_wv = 8 * 32 * (TN * 16 + 4) * 4;
     constexpr int epi = epi_wg > epi_wv ? epi_wg : epi_wv;
     return ring > epi ? ring : epi;
 }
 
-// (output width, 16-row tiles per wave) of row-ring tile `id` (42 / 43 / 44), or {0, 0}
-struct RrTile { int id, w, tmw; };
-constexpr RrTile kRrTiles[] = {{42, 64, 8}, {43, 32, 4}, {44, 16, 4}};
+// (output width, 16-row tiles per wave, row groups) of row-ring tile `id`
+struct RrTile { int id, w, tmw, nrg; };
+constexpr RrTile kRrTiles[] = {{42, 64, 8, 2}, {43, 32, 4, 2}, {44, 16, 4, 2}};
 
 // A row-ring tile applies to: 3x3, stride 1, a single zero-bordered source (src_pad: the host
 // maps it to a valid conv, pad 0, over the padded image), 64-channel blocks, output width W
@@ -353,14 +385,14 @@ __host__ __device__ constexpr int pp16r_tile_for(int ksize, int stride, int pad,
                                                  int w) {
     if (!(ksize == 3 && stride == 1 && pad == 0 && c1 == 0 && cin % 64 == 0 && w == ow + 2)) return 0;
     for (const RrTile& t : kRrTiles)
-        if (ow == t.w && (oh * ow) % (2 * t.tmw * 16) == 0) return t.id;
+        if (ow == t.w && (oh * ow) % (t.nrg * t.tmw * 16) == 0) return t.id;   // the first (preferred) tile
     return 0;
 }
 
-template <int TN, int W, int TMW, int PH, int NB>
+template <int TN, int W, int TMW, int PH, int NB, int NRG = 2>
 static void run_pp16r_t(IgemmParams& p, hipStream_t s) {
-    constexpr int BN = 4 * TN * 16, BM = 2 * TMW * 16;
-    constexpr int smem = pp16r_smem<TN, W, TMW, NB>();
+    constexpr int BN = (8 / NRG) * TN * 16, BM = NRG * TMW * 16;
+    constexpr int smem = pp16r_smem<TN, W, TMW, NB, NRG>();
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
     p.gx = (p.cout + BN - 1) / BN;
     p.gy = p.M / BM;
@@ -371,8 +403,8 @@ static void run_pp16r_t(IgemmParams& p, hipStream_t s) {
     if (cbs > ncb) cbs = ncb;
     p.ksplit = (ncb + cbs - 1) / cbs;
     p.nkt = 9 * cbs;
-    ensure_lds<igemm_pp16r_kernel<TN, PH, W, TMW, NB>>(smem);
-    hipLaunchKernelGGL((igemm_pp16r_kernel<TN, PH, W, TMW, NB>), dim3(p.gx * p.gy * p.ksplit), dim3(512), smem, s, p);
+    ensure_lds<igemm_pp16r_kernel<TN, PH, W, TMW, NB, NRG>>(smem);
+    hipLaunchKernelGGL((igemm_pp16r_kernel<TN, PH, W, TMW, NB, NRG>), dim3(p.gx * p.gy * p.ksplit), dim3(512), smem, s, p);
     if (p.ksplit > 1) run_splitk_reduce(p, s);
 }
 

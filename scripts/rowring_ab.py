@@ -13,13 +13,13 @@ import torch.nn.functional as F
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from clap2diffusion_amd import ops  # noqa: E402
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--batch", type=int, default=8)
-ap.add_argument("--iters", type=int, default=20)
-ap.add_argument("--only", default="")
-a = ap.parse_args()
-dev = torch.device("cuda")
-N = 2 * a.batch
+SHAPES_C2 = [  # N = 2 (c2): the planner's table plans against the row-ring tiles with split K
+    ("c2 L0 3x3 320 +res", 64, 320, 320, "resid", [(7, 4), (42, 5), (42, 3)]),
+    ("c2 L0 3x3 960->320 +temb", 64, 960, 320, "temb", [(40, 8), (42, 8), (42, 15)]),
+    ("c2 L1 3x3 640 +res", 32, 640, 640, "resid", [(7, 8), (43, 4), (43, 8), (43, 10)]),
+    ("c2 L1 3x3 1920->640 +temb", 32, 1920, 640, "temb", [(40, 16), (43, 8), (43, 15)]),
+    ("c2 L2 3x3 1280 +res", 16, 1280, 1280, "resid", [(7, 12), (44, 8), (44, 10), (44, 20)]),
+]
 SHAPES = [  # name, h, cin, cout, form, plans to force (tile, split)
     ("L0 3x3 320 +res", 64, 320, 320, "resid", [(40, 1), (42, 1)]),
     ("L1 3x3 640 +res", 32, 640, 640, "resid", [(40, 2), (43, 1), (43, 2), (7, 1)]),
@@ -62,45 +62,57 @@ def timed(fn, iters):
     return best
 
 
-for name, h, cin, cout, form, plans in SHAPES:
-    if a.only and a.only not in name:
-        continue
-    x = gen(N, cin, h, h, seed=1)
-    w = gen(cout, cin, 3, 3, seed=2, scale=1 / math.sqrt(9 * cin))
-    b = gen(cout, seed=3) * 0.1
-    ref = F.conv2d(x, w, b, padding=1)
-    temb = resid = None
-    if form == "temb":
-        temb = gen(N, cout, seed=4)
-        ref = ref + temb[:, :, None, None]
-    else:
-        resid = gen(N, cout, h, h, seed=5)
-        ref = ref + resid
-    xp = torch.zeros(N, h + 2, h + 2, cin)
-    xp[:, 1:-1, 1:-1] = x.permute(0, 2, 3, 1)
-    xp = xp.half().to(dev)
-    wp, kp = ops.pack_conv_weight(w)
-    wp, bd = wp.to(dev), b.float().to(dev)
-    td = None if temb is None else temb.half().to(dev)
-    rd = None if resid is None else resid.permute(0, 2, 3, 1).contiguous().half().to(dev)
-    out = torch.empty(N, h, h, cout, dtype=torch.float16, device=dev)
-    refn = ref.permute(0, 2, 3, 1).to(dev)
-    for pl in [None] + plans:
-        def run():
-            ops.conv(xp, wp, kp, cout, ksize=3, bias=bd, padded=True, temb=td, resid=rd, out=out)
-        try:
-            if pl is None:
-                with ops.record_conv_plans() as rec:
-                    run()
-                us = timed(run, a.iters)
-            else:
-                with ops.force_plan(*pl):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="", help="comma-separated name substrings")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    N = 2 * a.batch
+    for name, h, cin, cout, form, plans in (SHAPES_C2 if a.batch == 1 else SHAPES):
+        if a.only and not any(o in name for o in a.only.split(",")):
+            continue
+        x = gen(N, cin, h, h, seed=1)
+        w = gen(cout, cin, 3, 3, seed=2, scale=1 / math.sqrt(9 * cin))
+        b = gen(cout, seed=3) * 0.1
+        ref = F.conv2d(x, w, b, padding=1)
+        temb = resid = None
+        if form == "temb":
+            temb = gen(N, cout, seed=4)
+            ref = ref + temb[:, :, None, None]
+        else:
+            resid = gen(N, cout, h, h, seed=5)
+            ref = ref + resid
+        xp = torch.zeros(N, h + 2, h + 2, cin)
+        xp[:, 1:-1, 1:-1] = x.permute(0, 2, 3, 1)
+        xp = xp.half().to(dev)
+        wp, kp = ops.pack_conv_weight(w)
+        wp, bd = wp.to(dev), b.float().to(dev)
+        td = None if temb is None else temb.half().to(dev)
+        rd = None if resid is None else resid.permute(0, 2, 3, 1).contiguous().half().to(dev)
+        out = torch.empty(N, h, h, cout, dtype=torch.float16, device=dev)
+        refn = ref.permute(0, 2, 3, 1).to(dev)
+        for pl in [None] + plans:
+            def run():
+                ops.conv(xp, wp, kp, cout, ksize=3, bias=bd, padded=True, temb=td, resid=rd, out=out)
+            try:
+                if pl is None:
                     with ops.record_conv_plans() as rec:
                         run()
                     us = timed(run, a.iters)
-        except Exception as e:  # noqa: BLE001
-            print(f"{name:28s} {str(pl):10s} failed: {e}", flush=True)
-            continue
-        err = ((out.float() - refn).norm() / refn.norm()).item()
-        tag = "planner" if pl is None else "forced"
-        print(f"{name:28s} {tag:8s} {str(rec[0]):10s} {us:8.1f} us  rel-L2 {err:.2e}", flush=True)
+                else:
+                    with ops.force_plan(*pl):
+                        with ops.record_conv_plans() as rec:
+                            run()
+                        us = timed(run, a.iters)
+            except Exception as e:  # noqa: BLE001
+                print(f"{name:28s} {str(pl):10s} failed: {e}", flush=True)
+                continue
+            err = ((out.float() - refn).norm() / refn.norm()).item()
+            tag = "planner" if pl is None else "forced"
+            print(f"{name:28s} {tag:8s} {str(rec[0]):10s} {us:8.1f} us  rel-L2 {err:.2e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
