@@ -21,7 +21,7 @@ ERRORS = {-1: "C2D_E_ARG", -2: "C2D_E_SHAPE", -3: "C2D_E_ALIGN", -4: "C2D_E_HIP"
 
 # every symbol include/c2d.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "c2d_conv2d_igemm", "c2d_conv2d_igemm_workspace_size", "c2d_conv2d_igemm_plan", "c2d_set_plan_override", "c2d_get_plan_override", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_groupnorm_run_workspace_size", "c2d_groupnorm", "c2d_groupnorm_pad_workspace_size", "c2d_groupnorm_pad", "c2d_layernorm_stats",
+    "c2d_conv2d_igemm", "c2d_conv2d_igemm_workspace_size", "c2d_conv2d_igemm_plan", "c2d_set_plan_override", "c2d_get_plan_override", "c2d_groupnorm_workspace_size", "c2d_groupnorm_stats", "c2d_groupnorm_apply", "c2d_groupnorm_run_workspace_size", "c2d_groupnorm", "c2d_groupnorm_pad_workspace_size", "c2d_groupnorm_pad", "c2d_conv2d_gn_rows", "c2d_groupnorm_moments", "c2d_layernorm_stats",
     "c2d_layernorm", "c2d_attention_fwd", "c2d_attention_fwd_bias", "c2d_attention_fwd_mask", "c2d_window_attention", "c2d_htsat_mel_patches",
     "c2d_patch_merge_gather", "c2d_row_mean", "c2d_l2_normalize", "c2d_softmax_rows", "c2d_clap_log_mel", "c2d_attention_small", "c2d_pack_weights", "c2d_timestep_embedding",
     "c2d_cfg_ddim_step", "c2d_latent_to_nhwc", "c2d_upsample_nearest2x", "c2d_add", "c2d_last_hip_error", "c2d_version",
@@ -39,6 +39,7 @@ class ConvDesc(ctypes.Structure):
         ("temb", c_void_p), ("temb_ld", c_int), ("resid", c_void_p), ("resid_ld", c_int),
         ("out", c_void_p), ("out_ld", c_int), ("ws", c_void_p), ("ws_bytes", c_size_t),
         ("src_pad", c_int), ("pro_eps", c_float),
+        ("gn_mom", c_void_p), ("gn_groups", c_int),   # r6: producer-emitted GroupNorm moments
     ]
 
 
@@ -68,6 +69,8 @@ def lib() -> ctypes.CDLL:
         "c2d_groupnorm": ([vp, vp, i, i, i, i, i, f, vp, vp, i, vp, vp, sz, vp], i),
         "c2d_groupnorm_pad_workspace_size": ([i, i, i, i], sz),
         "c2d_groupnorm_pad": ([vp, vp, i, i, i, i, i, i, f, vp, vp, i, vp, vp, sz, vp], i),
+        "c2d_conv2d_gn_rows": ([ctypes.POINTER(ConvDesc)], i),
+        "c2d_groupnorm_moments": ([vp, i, i, i, i, f, vp, vp, i, vp, i, i, vp, vp], i),
         "c2d_layernorm_stats": ([vp, i, i, i, f, vp, vp], i),
         "c2d_layernorm": ([vp, i, i, i, f, vp, vp, vp, i, vp], i),
         "c2d_attention_fwd": ([vp, i, vp, i, vp, i, vp, i, i, i, i, i, i, f, i, vp], i),

@@ -24,7 +24,9 @@ namespace c2d {
 // NT: threads sharing the image (64: a wave's own image; 512: a workgroup image).
 // RG: 0 = image row r is output row m0 + r; else the image holds groups of 32 rows whose
 // output rows lie RG apart (m0 + (r / 32) RG + r % 32: the row groups of a 2-row-group tile).
-template <int W, bool GG, int ROWS, int COLS, int RES, int TEMB, int NT = 64, int RG = 0>
+// WB: also write each stored value (as rounded to fp16) back over its image entry, so that a pass
+// over the image afterwards sees exactly the output (epi_pass_wb: the producer-side GroupNorm moments)
+template <int W, bool GG, int ROWS, int COLS, int RES, int TEMB, int NT = 64, int RG = 0, bool WB = false>
 struct EpiPass {
     typedef _Float16 hv __attribute__((ext_vector_type(W)));
     static constexpr int CPR = GG ? COLS / (2 * W) : COLS / W;   // W-wide output chunks per row
@@ -115,6 +117,12 @@ struct EpiPass {
 #pragma unroll
         for (int q = 0; q < W; ++q) o[q] = (f16)v[q];
         if (ok) *reinterpret_cast<hv*>(p.out + (size_t)m * p.out_ld + j) = o;
+        if constexpr (WB) {
+            float* dst = const_cast<float*>(src);
+#pragma unroll
+            for (int q = 0; q < W; q += 4)
+                *reinterpret_cast<float4*>(dst + q) = make_float4((float)o[q], (float)o[q + 1], (float)o[q + 2], (float)o[q + 3]);
+        }
     }
 
     __device__ __forceinline__ void finish(const IgemmParams& p, const float* img, int pitchf, int m0, int jp0,
@@ -182,6 +190,72 @@ __device__ __forceinline__ void epi_pass_t(const IgemmParams& p, const float* im
         ep.finish(p, img, pitchf, m0, jp0, lane);
     }
     sync();       // image reads done before the next pass rewrites it
+}
+
+// One compact workgroup pass (16-B outputs, no GEGLU: the caller checked) that leaves the stored
+// values in the image and runs after() over it before the next pass may rewrite it
+template <int NT, int RG, int ROWS, int COLS, class WriteImg, class After>
+__device__ __forceinline__ void epi_pass_wb(const IgemmParams& p, const float* img, int pitchf, int m0, int jp0,
+                                            int lane, WriteImg&& write_img, After&& after) {
+    typedef EpiPass<8, false, ROWS, COLS, -1, -1, NT, RG, true> EP;
+    auto sync = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));   // lgkmcnt(0)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    write_img();
+    sync();
+    EP::compact(p, img, pitchf, m0, jp0, lane);
+    sync();
+    after();
+    sync();
+}
+
+// GroupNorm moments of a BM x BN output tile (IgemmParams::gn_mom) from its workgroup-image epilogue: NPASS
+// epi_pass_wb passes of ROWS image rows (image row r = output row m0 + 16 * 2 pass + (r / 32) RG + r % 32),
+// write_img(pass) writing pass's bias-added accumulators.  Each pass leaves its stored fp16 values in the
+// image; thread c < BN then adds column n0 + c's values, shifted by the tile's first one, over the pass's rows.
+// At the end: per column (mean, M2) over the BM rows -> LDS -> per group (fixed channel order, equal counts)
+// -> {mean, M2} of (image, tile, group).  Needs BM-row tiles inside one image, BN % cpg == 0, n0 % cpg == 0.
+template <int NPASS, int ROWS, int BN, int BM, int RG, class WriteImg>
+__device__ __forceinline__ void epi_gn_moments(const IgemmParams& p, float* img, int pitchb, int m0, int n0, int tid,
+                                               WriteImg&& write_img) {
+    float sh = 0.f, s1 = 0.f, s2 = 0.f;
+    static_for<0, NPASS>([&](auto pass) __attribute__((always_inline)) {
+        constexpr int b0 = 2 * decltype(pass)::value;
+        epi_pass_wb<512, RG, ROWS, BN>(p, img, pitchb, m0 + b0 * 16, n0, tid,
+                                       [&]() __attribute__((always_inline)) { write_img(pass); },
+                                       [&]() __attribute__((always_inline)) {
+            if (tid < BN) {
+                if constexpr (b0 == 0) sh = img[tid];
+#pragma unroll 8
+                for (int r = 0; r < ROWS; ++r) {
+                    const float d = img[r * pitchb + tid] - sh;
+                    s1 += d;
+                    s2 = fmaf(d, d, s2);
+                }
+            }
+        });
+    });
+    float2* chm = reinterpret_cast<float2*>(img);   // the image is free again (epi_pass_wb's last barrier)
+    if (tid < BN) chm[tid] = make_float2(sh + s1 * (1.0f / BM), s2 - s1 * s1 * (1.0f / BM));
+    __syncthreads();
+    const int cpg = p.gn_cpg, ng = BN / cpg;
+    if (tid < ng) {
+        float mg = 0.f;
+        for (int i = 0; i < cpg; ++i) mg += chm[tid * cpg + i].x;
+        mg /= (float)cpg;
+        float q = 0.f;
+        for (int i = 0; i < cpg; ++i) {
+            const float2 e = chm[tid * cpg + i];
+            const float d = e.x - mg;
+            q += e.y + (float)BM * d * d;
+        }
+        const int hw = p.oh * p.ow, nimg = m0 / hw, tpi = hw / BM, groups = p.cout / cpg;
+        const size_t slot = ((size_t)nimg * tpi + (m0 - nimg * hw) / BM) * groups + n0 / cpg + tid;
+        reinterpret_cast<float2*>(p.gn_mom)[slot] = make_float2(mg, q);
+    }
 }
 
 // ROWS x COLS image pass -> outputs; picks the 16-B (W = 8) form when the output

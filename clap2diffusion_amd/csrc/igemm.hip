@@ -57,6 +57,8 @@ struct IgemmParams {
     int lds_epi; // 32x32 kernels: 1 = LDS-staged epilogue (C2D_TUNE_GEMM_LDSEPI or alignment), 0 = direct
     int cmajor;  // DMA 3x3 kernels: K steps channel-block-outer / tap-inner (C2D_TUNE_GEMM_KORDER, default 1)
     float pro_eps;   // C2D_PRO_LNFOLD: LayerNorm eps
+    float* gn_mom;   // GroupNorm moments of the output ({mean, M2} per (image, tile, group)) or NULL (row-ring tiles only)
+    int gn_cpg;      // channels per group of gn_mom
 };
 
 // one accumulator quad of K slice `slice` into the split-K workspace, fp32 or rounded to fp16
@@ -449,18 +451,26 @@ __device__ __forceinline__ void epilogue_chunked(const IgemmParams& p, f32x4 (&a
     }
 }
 
-template <int WM, int WN, int TM, int TN, int STAGES, int KS>
-__global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) {
+// KG > 1: intra-workgroup split-K.  KG groups of WM x WN waves share the output tile, group g
+// walking its own contiguous share of the block's K steps through its own STAGES-slot ring;
+// after the loop groups 1 .. KG-1 leave their raw accumulators in LDS (lane-linear, fixed
+// order) and exit, group 0 adds them and runs the epilogue (or the split-K slab store).  Two
+// waves per SIMD on the under-filled grids (level-2 / level-3 GEMMs: one 4-wave tile per CU)
+// with no fp32 slab traffic and no combine launch.
+template <int WM, int WN, int TM, int TN, int STAGES, int KS, int KG = 1>
+__global__ void __launch_bounds__(64 * WM * WN * KG) igemm_dma_kernel(IgemmParams p) {
     constexpr int NW = WM * WN;
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);   // DMA pieces per wave per stage
     constexpr int PER = AI + BI;
     constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
     static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave mismatch");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+    extern __shared__ __attribute__((aligned(16))) char smem_all[];
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kg = wave_all / NW, wave = wave_all - kg * NW;   // K group, wave within the group
+    char* const smem = smem_all + (KG > 1 ? kg * STAGES * STAGE : 0);
     const int wm = wave / WN, wn = wave - (wave / WN) * WN;
     // block -> (output tile, K slice); the remap keeps a tile's slices on one XCD
     const int bid = xcd_remap(blockIdx.x, p.gx * p.gy * p.ksplit);
@@ -512,7 +522,9 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     const bool ctail = (p.cin & 63) != 0;
 
     const int nk_all = p.kpad / 64;
-    const int kb = slice * p.nkt, ke = min(nk_all, kb + p.nkt);   // this block's K steps [kb, ke)
+    const int kb0 = slice * p.nkt, ke0 = min(nk_all, kb0 + p.nkt);   // this block's K steps [kb0, ke0)
+    const int kper = (ke0 - kb0 + KG - 1) / KG;                      // steps per K group (the loop count)
+    const int kb = min(ke0, kb0 + kg * kper), ke = min(ke0, kb + kper);   // this group's share
     const char* u_src0 = uniform_ptr(p.src0);
     const char* u_src1 = uniform_ptr(p.src1);
     const char* u_wt = uniform_ptr(p.wt);
@@ -575,7 +587,10 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
         if (kb + s0 < ke) issue(kb + s0, s0);
     int rd = 0, wr = STAGES - 1;
-    for (int kt = kb; kt < ke; ++kt) {
+    // every group runs kper trips (the barriers are workgroup-wide); a group with fewer steps
+    // (the last share of an odd count) idles through its surplus trips
+    const int kend = KG > 1 ? kb + kper : ke;
+    for (int kt = kb; kt < kend; ++kt) {
         if (kt + STAGES - 2 < ke) wait_vmcnt_le(PER * (STAGES - 2));
         else wait_vmcnt_le(0);
         asm volatile("" ::: "memory");
@@ -585,6 +600,7 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         // prologue stages, bit 1 skips the MFMAs (fragments still read and kept live)
         if (kt + STAGES - 1 < ke && !(C2D_ABL(p.abl, 1))) issue(kt + STAGES - 1, wr);
         const char* S = smem + rd * STAGE;
+        if (KG > 1 && kt >= ke) continue;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             f16x8 fa[TM], fb[TN];
@@ -609,6 +625,28 @@ __global__ void __launch_bounds__(64 * WM * WN) igemm_dma_kernel(IgemmParams p) 
         }
         rd = (rd + 1 == STAGES) ? 0 : rd + 1;
         wr = (wr + 1 == STAGES) ? 0 : wr + 1;
+    }
+    if constexpr (KG > 1) {
+        // groups 1 .. KG-1 -> LDS (above the epilogue images), group 0 adds them in group order
+        constexpr int EPI = NW * 16 * (TM < 2 ? TM : 2) * (TN * 16 + 4) * 4;
+        constexpr int RED = (EPI + 1023) / 1024 * 1024;
+        f32x4* red = reinterpret_cast<f32x4*>(smem_all + RED);
+        __syncthreads();   // every group is done with its ring
+        if (kg > 0) {
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b)
+                    red[((((kg - 1) * NW + wave) * TN + a) * TM + b) * 64 + lane] = acc[a][b];
+        }
+        __syncthreads();
+        if (kg > 0) return;   // s_barrier waits only on the surviving waves from here on
+#pragma unroll
+        for (int g = 1; g < KG; ++g)
+#pragma unroll
+            for (int a = 0; a < TN; ++a)
+#pragma unroll
+                for (int b = 0; b < TM; ++b) acc[a][b] += red[((((g - 1) * NW + wave) * TN + a) * TM + b) * 64 + lane];
     }
     if (p.ksplit > 1) {
         // raw fp32 partial sums; bias / act / temb / residual go in splitk_reduce_kernel
@@ -718,7 +756,114 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
     *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
 }
 
+// Split-K combine that also emits the output's GroupNorm moments (IgemmParams::gn_mom): block = kGnRb rows x
+// 320 columns of one image, 320 threads; thread t owns columns 4 (t % 80) .. +3 and rows t / 80, + 4, ...
+// (kGnRb / 4 of them).  Each output goes through splitk_reduce_kernel's arithmetic; the thread keeps its
+// fp16-rounded values and forms their exact (mean, M2) per column (two passes in registers), the four row
+// threads of a column merge in LDS (Chan, equal counts, fixed order), then each group's columns.  Writes
+// {mean, M2} per (image, kGnRb-row block, group): the layout c2d_groupnorm_moments reads.
+constexpr int kGnRb = 32;
+template <int KS, bool S16>
+__global__ void __launch_bounds__(320) splitk_reduce_gn_kernel(IgemmParams p) {
+    constexpr int RPT = kGnRb / 4;
+    __shared__ float2 cm[4][320];
+    const int t = threadIdx.x, q = t % 80, rs = t / 80;
+    const int m0 = blockIdx.x * kGnRb, j = blockIdx.y * 320 + 4 * q;
+    const int hw = p.oh * p.ow;
+    const size_t slab = (size_t)p.M * p.cout;
+    float4 bv = {0.f, 0.f, 0.f, 0.f};
+    f16x4 tv = {0, 0, 0, 0};
+    if (p.bias) bv = *reinterpret_cast<const float4*>(p.bias + j);
+    if (p.temb) tv = *reinterpret_cast<const f16x4*>(p.temb + (size_t)(m0 / hw) * p.temb_ld + j);
+    float y[RPT][4];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int m = m0 + rs + 4 * i;
+        const size_t src = (size_t)m * p.cout + j;
+        f32x4 v[KS];
+#pragma unroll
+        for (int sl = 0; sl < KS; ++sl) v[sl] = slab_quad<S16>(p.ws, src + sl * slab);
+        f32x4 acc = v[0];
+#pragma unroll
+        for (int sl = 1; sl < KS; ++sl) acc += v[sl];
+        f16x4 rv = {0, 0, 0, 0};
+        if (p.resid) rv = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
+        f16x4 o;
+        const float b4[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float x = acc[r] + b4[r];
+            if (p.temb) x += (float)tv[r];
+            if (p.resid) x += (float)rv[r];
+            o[r] = (f16)x;
+            y[i][r] = (float)o[r];
+        }
+        *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float mu = 0.f;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) mu += y[i][r];
+        mu *= 1.0f / RPT;
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) m2 = fmaf(y[i][r] - mu, y[i][r] - mu, m2);
+        cm[rs][4 * q + r] = make_float2(mu, m2);
+    }
+    __syncthreads();
+    const int cpg = p.gn_cpg, ng = 320 / cpg;
+    {   // per column t: merge the four row threads (equal counts RPT)
+        float mu = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mu += cm[k][t].x;
+        mu *= 0.25f;
+        float m2 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float d = cm[k][t].x - mu;
+            m2 += cm[k][t].y + (float)RPT * d * d;
+        }
+        __syncthreads();
+        cm[0][t] = make_float2(mu, m2);
+    }
+    __syncthreads();
+    if (t < ng) {   // per group: its columns (equal counts kGnRb)
+        float mg = 0.f;
+        for (int i = 0; i < cpg; ++i) mg += cm[0][t * cpg + i].x;
+        mg /= (float)cpg;
+        float m2 = 0.f;
+        for (int i = 0; i < cpg; ++i) {
+            const float d = cm[0][t * cpg + i].x - mg;
+            m2 += cm[0][t * cpg + i].y + (float)kGnRb * d * d;
+        }
+        const int nimg = m0 / hw, groups = p.cout / cpg;
+        const size_t slot = ((size_t)nimg * (hw / kGnRb) + (m0 - nimg * hw) / kGnRb) * groups + blockIdx.y * ng + t;
+        reinterpret_cast<float2*>(p.gn_mom)[slot] = make_float2(mg, m2);
+    }
+}
+
 void run_splitk_reduce(const IgemmParams& p, hipStream_t s) {
+    if (p.gn_mom) {   // gn_rows_for: cout % 320 == 0, hw % kGnRb == 0, act none
+        const dim3 grid((unsigned)(p.M / kGnRb), (unsigned)(p.cout / 320)), blk(320);
+#define C2D_SKG(KS)                                                                                    \
+    if (p.slab16) hipLaunchKernelGGL((splitk_reduce_gn_kernel<KS, true>), grid, blk, 0, s, p);        \
+    else hipLaunchKernelGGL((splitk_reduce_gn_kernel<KS, false>), grid, blk, 0, s, p)
+        switch (p.ksplit) {
+            case 2: C2D_SKG(2); break;
+            case 3: C2D_SKG(3); break;
+            case 4: C2D_SKG(4); break;
+            case 5: C2D_SKG(5); break;
+            case 6: C2D_SKG(6); break;
+            case 8: C2D_SKG(8); break;
+            case 10: C2D_SKG(10); break;
+            case 12: C2D_SKG(12); break;
+            case 15: C2D_SKG(15); break;
+            default: C2D_SKG(16); break;   // gn_split_ok: only the counts above and 16
+        }
+#undef C2D_SKG
+        return;
+    }
     const size_t total = (size_t)p.M * (p.cout >> 2);
     const dim3 grid((unsigned)((total + 255) / 256)), blk(256);
 #define C2D_SKR(KS)                                                                   \
@@ -748,17 +893,19 @@ void run_splitk_reduce(const IgemmParams& p, hipStream_t s);
 #include "igemm_panel.h"
 namespace c2d {
 
-template <int WM, int WN, int TM, int TN, int STAGES, int KS>
+template <int WM, int WN, int TM, int TN, int STAGES, int KS, int KG = 1>
 static void launch_dma(const IgemmParams& p, hipStream_t s) {
-    // the ring, or the fp32 epilogue image (per wave 16 * min(TM, 2) rows x (TN * 16 + 4)
-    // floats) that reuses it after the main loop, whichever is larger
-    constexpr int ring = STAGES * (WM * TM + WN * TN) * 16 * 128;
-    constexpr int epi = WM * WN * 16 * (TM < 2 ? TM : 2) * (TN * 16 + 4) * 4;
+    // the KG rings, or the fp32 epilogue image (per wave 16 * min(TM, 2) rows x (TN * 16 + 4)
+    // floats) that reuses them after the main loop (KG > 1: plus the other groups' accumulators
+    // above it), whichever is larger
+    constexpr int ring = KG * STAGES * (WM * TM + WN * TN) * 16 * 128;
+    constexpr int epi0 = WM * WN * 16 * (TM < 2 ? TM : 2) * (TN * 16 + 4) * 4;
+    constexpr int epi = KG > 1 ? (epi0 + 1023) / 1024 * 1024 + (KG - 1) * WM * WN * TM * TN * 1024 : epi0;
     constexpr int smem = ring > epi ? ring : epi;
     static_assert(smem <= 160 * 1024, "LDS ring / epilogue image too large");
-    auto k = igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>;
-    ensure_lds<igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS>>(smem);
-    hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN), smem, s, p);
+    auto k = igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS, KG>;
+    ensure_lds<igemm_dma_kernel<WM, WN, TM, TN, STAGES, KS, KG>>(smem);
+    hipLaunchKernelGGL(k, dim3(p.gx * p.gy * p.ksplit), dim3(64 * WM * WN * KG), smem, s, p);
     if (p.ksplit > 1) run_splitk_reduce(p, s);
 }
 
@@ -781,13 +928,13 @@ static int gemm_mode() { return tuning().gemm_mode; }
 // per-tile parity test); 0 = heuristic.  An explicit setter, never the environment.
 static int gemm_tile() { return plan_override_tile(); }
 
-template <int WM, int WN, int TM, int TN, int ST>
+template <int WM, int WN, int TM, int TN, int ST, int KG = 1>
 static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     p.gx = (cout + BN - 1) / BN;
     p.gy = (p.M + BM - 1) / BM;
-    if (ksize == 1) launch_dma<WM, WN, TM, TN, ST, 1>(p, s);
-    else launch_dma<WM, WN, TM, TN, ST, 3>(p, s);
+    if (ksize == 1) launch_dma<WM, WN, TM, TN, ST, 1, KG>(p, s);
+    else launch_dma<WM, WN, TM, TN, ST, 3, KG>(p, s);
 }
 
 // One wrapper per DMA tile id, each compiled in its kernel family's part.
@@ -795,7 +942,7 @@ static void run_dma(IgemmParams& p, int ksize, int cout, hipStream_t s) {
 namespace c2d {
 C2D_TILE_FN(25); C2D_TILE_FN(40); C2D_TILE_FN(41); C2D_TILE_FN(28); C2D_TILE_FN(29);
 C2D_TILE_FN(7); C2D_TILE_FN(1); C2D_TILE_FN(2); C2D_TILE_FN(3); C2D_TILE_FN(50); C2D_TILE_FN(8); C2D_TILE_FN(9);
-C2D_TILE_FN(42); C2D_TILE_FN(43); C2D_TILE_FN(44); C2D_TILE_FN(70);
+C2D_TILE_FN(42); C2D_TILE_FN(43); C2D_TILE_FN(44); C2D_TILE_FN(70); C2D_TILE_FN(80); C2D_TILE_FN(81);
 #if C2D_PART(1)
 C2D_TILE_FN(40) { run_pp16<5>(p, ksize, cout, s); }   // 256x320 ping-pong 16x16x32
 C2D_TILE_FN(41) { run_pp16<4>(p, ksize, cout, s); }   // 256x256 ping-pong 16x16x32
@@ -816,6 +963,8 @@ C2D_TILE_FN(2) { run_dma<2, 2, 4, 4, 3>(p, ksize, cout, s); }   // 128x128, 4 wa
 C2D_TILE_FN(3) { run_dma<2, 2, 2, 2, 3>(p, ksize, cout, s); }   // 64x64, 4 waves of 32x32
 C2D_TILE_FN(8) { run_dma<2, 2, 4, 5, 2>(p, ksize, cout, s); }   // 128x160, 4 waves of 64x80, 72 KiB: 2 per CU
 C2D_TILE_FN(9) { run_dma<2, 2, 2, 5, 2>(p, ksize, cout, s); }   // 64x160, 4 waves of 32x80, 56 KiB: 2 per CU
+C2D_TILE_FN(80) { run_dma<2, 2, 4, 5, 2, 2>(p, ksize, cout, s); }   // 128x160, 2 K groups of 4 waves of 64x80, 144 KiB
+C2D_TILE_FN(81) { run_dma<2, 2, 2, 5, 2, 2>(p, ksize, cout, s); }   // 64x160, 2 K groups of 4 waves of 32x80, 112 KiB
 #endif
 #if C2D_PART(4)
 C2D_TILE_FN(70) { (void)ksize; (void)cout; run_panel(p, s); }   // 128-row A panel in LDS, weights streamed per wave
@@ -846,6 +995,9 @@ static const DmaTile kDmaTiles[] = {
     // two workgroups per CU (<= 80 KiB of LDS): the under-filled 1x1 / 3x3 shapes
     {8, 128, 160, 2, 0.0f, false},
     {9, 64, 160, 2, 0.0f, false},
+    // tiles 8 / 9 with two K groups in one workgroup (intra-workgroup split-K, 8 waves, one per CU)
+    {80, 128, 160, 1, 0.0f, false},
+    {81, 64, 160, 1, 0.0f, false},
     // row-ring 3x3 over a zero-bordered source (igemm_pp16r.h), one per output width (64 / 32 / 16):
     // chosen by plan_for only
     {42, 256, 320, 1, 0.0f, false},
@@ -947,8 +1099,9 @@ static const PlanHint kPlanHints[] = {
     {3, 512, 11520, 1280, false, 7, 12},      // 3x3 L2 1280: 55.2 -> 43.7 (split 12)
     {3, 512, 17280, 1280, false, 41, 16},     // 3x3 L2 1920 -> 1280: 75.2 -> 48.3
     {3, 512, 23040, 1280, false, 41, 16},     // 3x3 L2 2560 -> 1280: 95.4 -> 57.1
-    {3, 128, 11520, 1280, false, 3, 12},      // 3x3 L3 1280: 31.4 -> 25.7
-    {3, 128, 23040, 1280, false, 9, 16},      // 3x3 L3 2560 -> 1280: 52.6 -> 38.1
+    {3, 128, 11520, 1280, false, 81, 12},     // 3x3 L3 1280: 31.4 -> 25.7 (3, 12); r06 two K groups (81, 12): 23.8 -> 22.0
+    {3, 128, 23040, 1280, false, 81, 12},     // 3x3 L3 2560 -> 1280: 52.6 -> 38.1 (9, 16); r06 (81, 12): 36.4 -> 32.3
+    {1, 2048, 3200, 640, false, 81, 2},       // ff.net.2 + proj_out fold L1 (K = 5C): r06 (2, 3) 24.6 -> (81, 2) 22.9
     {1, 128, 6400, 1280, false, 3, 12},       // ff.net.2 + proj_out fold L3 (K = 5C): 15.0 -> 14.4
     // N = 8, 96^2 (c5)
     {1, 73728, 320, 320, false, 7, 1},        // 1x1 L0: 53.9 -> 41.6
@@ -961,6 +1114,7 @@ static const PlanHint kPlanHints[] = {
     {3, 18432, 5760, 640, false, 41, 1},      // 3x3 L1 640: 163.0 -> 147.7
     {3, 1152, 11520, 1280, false, 41, 8},     // 3x3 L3 1280: 65.4 -> 61.2
     {3, 1152, 23040, 1280, false, 41, 8},     // 3x3 L3 2560 -> 1280: 116.7 -> 96.1
+    {1, 1152, 6400, 1280, false, 80, 3},      // ff.net.2 + proj_out fold L3: r06 (7, 6) 41.6 -> (80, 3) 39.5
     {1, 73728, 1600, 320, false, 7, 1},       // ff.net.2 + proj_out fold L0: 145.6 -> 136.9
     {1, 18432, 3200, 640, false, 41, 1},      // fold L1: 121.9 -> 87.7
     // the panel GEMM (tile 70, igemm_panel.h), graph-replayed forced sweeps at the three batches
@@ -974,11 +1128,11 @@ static const PlanHint kPlanHints[] = {
     {1, 8192, 320, 960, false, 70, 1},        // c2 QKV L0: 13.9 -> 12.5
 #endif
     // N = 16, 64^2 (c3)
-    {1, 4096, 1280, 1280, false, 8, 1},       // 1x1 L2: 27.2 -> 24.5
+    {1, 4096, 1280, 1280, false, 80, 1},      // 1x1 L2: 27.2 -> 24.5 (8, 1); r06 two K groups (80, 1): +res 26.0 -> 24.9, plain 24.7 -> 22.9
     {1, 1024, 1280, 1280, false, 3, 1},       // 1x1 mid: 18.9 -> 13.5
     {3, 1024, 11520, 1280, false, 41, 12},    // 3x3 L3 1280: 61.2 -> 52.5 (r04 re-sweep, fp32 slabs)
     {3, 1024, 23040, 1280, false, 41, 12},    // 3x3 L3 2560 -> 1280: 97.2 -> 91.3 (split 8); 87.9 -> 77.3 (r04: 12)
-    {1, 4096, 6400, 1280, false, 7, 2},       // ff.net.2 + proj_out fold L2: 84.7 -> 82.2
+    {1, 4096, 6400, 1280, false, 80, 1},      // ff.net.2 + proj_out fold L2: 84.7 -> 82.2 (7, 2); r06 (80, 1): 82.2 -> 76.1
     // VAE decoder at batch 8 (profiles/r03_sweep_vae.txt): only the 1x1 shortcuts gain
     {1, 2097152, 256, 128, false, 1, 1},      // 512^2 256 -> 128: 511.9 -> 459.4
     {1, 524288, 512, 256, false, 1, 1},       // 256^2 512 -> 256: 307.5 -> 294.3
@@ -1153,6 +1307,8 @@ static void dispatch_dma(IgemmParams& p, const DmaPlan& pl, int ksize, int cout,
         case 2: return run_tile_2(p, ksize, cout, s);
         case 8: return run_tile_8(p, ksize, cout, s);
         case 9: return run_tile_9(p, ksize, cout, s);
+        case 80: return run_tile_80(p, ksize, cout, s);
+        case 81: return run_tile_81(p, ksize, cout, s);
         case 70: return run_tile_70(p, ksize, cout, s);
         default: return run_tile_3(p, ksize, cout, s);
     }
@@ -1240,6 +1396,46 @@ extern "C" size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d) {
     return pl.split > 1 ? (size_t)pl.split * M * d->cout * sizeof(float) : 0;
 }
 
+// Rows per GroupNorm-moment block of this descriptor's output as c2d_conv2d_igemm would run it, 0 =
+// the plan cannot emit moments.  One slice (after the workspace check the launch makes): the row-ring
+// tiles (42: 256 rows, 43 / 44: 128) and the 256 x 320 ping-pong tile 40 (256) through their
+// workgroup-image epilogue, which needs a residual or a time embedding; K split: the combine
+// (splitk_reduce_gn_kernel, kGnRb rows) at the slice counts it is built for.  Always: no
+// quantisation-tail split, act none, 16-B outputs, groups that tile the 320-column block
+static bool gn_split_ok(int ks) {   // the slice counts splitk_reduce_gn_kernel is built for
+    return ks == 2 || ks == 3 || ks == 4 || ks == 5 || ks == 6 || ks == 8 || ks == 10 || ks == 12 || ks == 15 || ks == 16;
+}
+
+static int gn_rows_for(const c2d_conv_desc* d) {
+    if (!d || d->gn_groups <= 0 || d->cout % d->gn_groups) return 0;
+    const int cpg = d->cout / d->gn_groups;
+    if (320 % cpg || d->cout % 320 || !(d->resid || d->temb) || d->act != C2D_ACT_NONE) return 0;
+    if ((d->out_ld & 7) || (d->resid && (d->resid_ld & 7)) || (d->temb && (d->temb_ld & 7)) || d->out_ld < d->cout) return 0;
+    if (((uintptr_t)d->out | (uintptr_t)d->resid | (uintptr_t)d->temb) & 15) return 0;
+    if (d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->kpad < 64 || !dma_eligible(d)) return 0;
+    const long M = (long)d->n * d->oh * d->ow;
+    DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
+    if (pl.id == 50 || pl.id == 70) return 0;   // the persistent / panel tiles never split and emit none
+    bool split = false;
+    if (pl.split > 1) {
+        const size_t need = (size_t)pl.split * M * d->cout * sizeof(float);
+        split = d->ws && d->ws_bytes >= need && aligned16(d->ws);   // else the launch runs one slice
+    }
+    if (d->n >= 2 && tail_images(d, pl)) return 0;
+    if (split) {   // the split-K combine emits them (splitk_reduce_gn_kernel), kGnRb-row blocks
+        if (pl.id == 42 || pl.id == 43 || pl.id == 44) {   // the row ring's slice count (run_pp16r_t)
+            const int ncb = d->c0 / 64, cbs = (pl.nkt + 8) / 9 < 1 ? 1 : ((pl.nkt + 8) / 9 > ncb ? ncb : (pl.nkt + 8) / 9);
+            pl.split = (ncb + cbs - 1) / cbs;
+        }
+        return gn_split_ok(pl.split) && ((long)d->oh * d->ow) % kGnRb == 0 ? kGnRb : 0;
+    }
+    if (pl.id == 40) return ((long)d->oh * d->ow) % 256 == 0 ? 256 : 0;   // ping-pong 256 x 320 (igemm_pp16.h)
+    if (pl.id != 42 && pl.id != 43 && pl.id != 44) return 0;
+    return pl.id == 42 ? 256 : 128;
+}
+
+extern "C" int c2d_conv2d_gn_rows(const c2d_conv_desc* d) { return gn_rows_for(d); }
+
 extern "C" int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit) {
     if (!d || !tile_id || !ksplit) return C2D_E_ARG;
     if (d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->cout <= 0 || d->kpad < 64) return C2D_E_SHAPE;
@@ -1270,6 +1466,8 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
 extern "C" int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream) {
     if (!d || !d->src0 || !d->weight || !d->out) return C2D_E_ARG;
     hipStream_t s = (hipStream_t)stream;
+    if (d->gn_mom && gn_rows_for(d) == 0) return C2D_E_SHAPE;   // moments requested of a plan that cannot emit them
+    if (d->gn_mom && ((uintptr_t)d->gn_mom & 7)) return C2D_E_ALIGN;
     if (d->n >= 2 && d->ksize >= 1 && d->oh > 0 && d->ow > 0 && d->cout > 0 && d->kpad >= 64 && dma_eligible(d)) {
         const long M = (long)d->n * d->oh * d->ow;
         const DmaPlan pl = plan_for(M, d->cout, d->kpad, d->act, pps_eligible(d), d->ksize, rr_eligible(d), panel_eligible(d));
@@ -1339,6 +1537,8 @@ static int conv_run(const c2d_conv_desc* d, hipStream_t s, const DmaPlan* fixed)
     p.resid = (const f16*)d->resid; p.resid_ld = d->resid_ld;
     p.out = (f16*)d->out; p.out_ld = d->out_ld;
     p.M = d->n * d->oh * d->ow;
+    p.gn_mom = (float*)d->gn_mom;   // c2d_conv2d_igemm checked gn_rows_for: a one-slice row-ring plan
+    p.gn_cpg = d->gn_mom ? d->cout / d->gn_groups : 0;
     if (p.M <= 0) return C2D_OK;
 
     const int amode = (d->ksize == 1) ? AM_1X1 : ((cin % 64) == 0 ? AM_3X3_FAST : AM_3X3_GEN);

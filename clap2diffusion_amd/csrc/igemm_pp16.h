@@ -184,6 +184,22 @@ __global__ void __launch_bounds__(512) igemm_pp16_kernel(IgemmParams p) {
             __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
             __builtin_amdgcn_wave_barrier();
         }
+    } else if (TN == 5 && p.gn_mom) {   // + the output's GroupNorm moments (tile 40; c2d_conv_desc::gn_mom)
+        constexpr int BN = 4 * TN * 16, PITCHB = BN + 4;
+        float* img = reinterpret_cast<float*>(smem);
+        const int wr0 = wr * 32, wc0 = wc * TN * 16;
+        epi_gn_moments<TMW / 2, 64, BN, BM, TMW * 16>(p, img, PITCHB, m0, n0, tid, [&](auto pass) __attribute__((always_inline)) {
+            constexpr int b0 = 2 * decltype(pass)::value;
+            f32x4 bv[TN];
+#pragma unroll
+            for (int a = 0; a < TN; ++a) bv[a] = bias4(p, nw0 + a * 16 + 4 * (lane >> 4));
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                for (int a = 0; a < TN; ++a)
+                    *reinterpret_cast<f32x4*>(img + (wr0 + bb * 16 + (lane & 15)) * PITCHB + wc0 + a * 16 +
+                                              4 * (lane >> 4)) = acc[a][b0 + bb] + bv[a];
+        });
     } else {
         constexpr int BN = 4 * TN * 16, PITCHB = BN + 4;
         float* img = reinterpret_cast<float*>(smem);

@@ -329,14 +329,19 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s
 // gn_finalize_kernel's per-channel affine for its own channels, then walks its pixels as
 // gn_apply_kernel does (PAD: the zero-bordered layout).  Same statistics in every workgroup of
 // an image: the fold order does not depend on the workgroup.
-template <int CPT, bool PAD>
+//
+// MOM: ws holds {mean, M2} per (image, block of mrows pixels, group) written by the producing conv
+// (c2d_conv_desc::gn_mom) instead of shifted sums: each of the `parts` threads of a group merges
+// every parts-th block (Chan's pairwise update, equal counts, fp64), then the group's thread merges
+// the parts in order.  Deterministic; no pass over the source for statistics.
+template <int CPT, bool PAD, bool MOM = false>
 __global__ void __launch_bounds__(256) gn_apply_fold_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
                                                             int c0, int c1, int hw, int cpg, int nblk, float eps,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ ws, int silu,
-                                                            f16* __restrict__ out, int pw = 0) {
-    __shared__ double dacc[512];   // [256][2] fold partials
+                                                            f16* __restrict__ out, int pw = 0, int mrows = 0) {
+    __shared__ double dacc[MOM ? 768 : 512];   // [256][2] fold partials (MOM: [256][3] count, mean, M2)
     __shared__ float gmr[512];     // [groups][2] mean, rstd (groups <= 256)
     const int cin = c0 + c1, nch = cin >> 3, groups = cin / cpg;
     const int L = nch < 256 ? nch : 256, R = 256 / L;
@@ -344,6 +349,41 @@ __global__ void __launch_bounds__(256) gn_apply_fold_kernel(const f16* __restric
     const int n = blockIdx.y;
     const size_t img = (size_t)n * hw;
     const int parts = 256 / groups;
+    if constexpr (MOM) {
+        const double nb = (double)mrows * cpg;   // values per block and group
+        if (t < parts * groups) {
+            const int g = t % groups, pt = t / groups;
+            const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * groups + g;
+            double na = 0.0, ma = 0.0, qa = 0.0;
+            for (int k = pt; k < nblk; k += parts) {
+                const float2 v = wp[(size_t)k * groups];
+                const double nn = na + nb, d = (double)v.x - ma;
+                ma += d * (nb / nn);
+                qa += (double)v.y + d * d * (na * nb / nn);
+                na = nn;
+            }
+            dacc[t * 3] = na;
+            dacc[t * 3 + 1] = ma;
+            dacc[t * 3 + 2] = qa;
+        }
+        __syncthreads();
+        if (t < groups) {
+            double na = 0.0, ma = 0.0, qa = 0.0;
+            for (int pt = 0; pt < parts; ++pt) {
+                const int u = (pt * groups + t) * 3;
+                const double nb2 = dacc[u];
+                if (nb2 == 0.0) continue;
+                const double nn = na + nb2, d = dacc[u + 1] - ma;
+                ma += d * (nb2 / nn);
+                qa += dacc[u + 2] + d * d * (na * nb2 / nn);
+                na = nn;
+            }
+            double var = qa / na;
+            if (var < 0.0) var = 0.0;
+            gmr[t * 2] = (float)ma;
+            gmr[t * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+    } else {
     if (t < parts * groups) {
         const int g = t % groups, pt = t / groups;
         const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * groups + g;
@@ -374,6 +414,7 @@ __global__ void __launch_bounds__(256) gn_apply_fold_kernel(const f16* __restric
         if (var < 0.0) var = 0.0;
         gmr[t * 2] = (float)(gn_read(s0, s1, c0, c1, img, t * cpg) + m1);
         gmr[t * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
+    }
     }
     __syncthreads();
     if (r0 >= R) return;
@@ -890,6 +931,36 @@ static int gn_fold_run(const void* src0, const void* src1, int c0, int c1, int n
         if (pw) C2D_GNF(2, true); else C2D_GNF(2, false);
     }
 #undef C2D_GNF
+    return check_launch();
+}
+
+extern "C" int c2d_groupnorm_moments(const void* src, int c, int n, int hw, int groups, float eps, const float* gamma,
+                                     const float* beta, int silu, const float* mom, int rows, int pw, void* out,
+                                     void* stream) {
+    if (!src || !gamma || !beta || !mom || !out) return C2D_E_ARG;
+    if ((c & 7) || c <= 0 || (c >> 3) > 512 || groups <= 0 || groups > 256 || c % groups || n <= 0 || hw <= 0)
+        return C2D_E_SHAPE;
+    if (rows <= 0 || hw % rows) return C2D_E_SHAPE;
+    if (pw && (pw < 3 || hw % (pw - 2))) return C2D_E_SHAPE;
+    if (!aligned16(src) || !aligned16(out) || ((uintptr_t)mom & 7)) return C2D_E_ALIGN;
+    const int nch = c >> 3, cpg = c / groups, nblk = hw / rows;
+    const int L = nch < 256 ? nch : 256, R = 256 / L;
+    const int npix = pw ? (hw / (pw - 2) + 2) * pw : hw;
+    int bx = ((n < 8 ? tuning().gn_fold_apply_blocks : gn_apply_blocks()) + n - 1) / n;   // as gn_fold_run
+    const int maxb = (npix + R - 1) / R;
+    if (bx > maxb) bx = maxb;
+    if (bx < 1) bx = 1;
+    const dim3 agrid(bx, n);
+    hipStream_t s = (hipStream_t)stream;
+#define C2D_GNM(C, PD)                                                                                            \
+    hipLaunchKernelGGL((gn_apply_fold_kernel<C, PD, true>), agrid, dim3(256), 0, s, (const f16*)src, (const f16*)nullptr, \
+                       c, 0, hw, cpg, nblk, eps, gamma, beta, mom, silu, (f16*)out, pw, rows)
+    if (nch <= 256) {
+        if (pw) C2D_GNM(1, true); else C2D_GNM(1, false);
+    } else {
+        if (pw) C2D_GNM(2, true); else C2D_GNM(2, false);
+    }
+#undef C2D_GNM
     return check_launch();
 }
 

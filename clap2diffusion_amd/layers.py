@@ -81,10 +81,11 @@ class HGroupNorm(nn.Module):
         return ops.group_norm_stats(x, self.num_groups, self.eps, self.weight, self.bias, x2=x2)
 
     def apply(self, x: torch.Tensor, x2: torch.Tensor | None = None, silu: bool = False,
-              pad: bool = False) -> torch.Tensor:
+              pad: bool = False, mom=None) -> torch.Tensor:
         """act(GroupNorm(cat[x, x2])) materialised once (c2d_groupnorm); pad: in the zero-bordered
-        layout a conv(..., padded=True) reads (c2d_groupnorm_pad)."""
-        return ops.group_norm(x, self.num_groups, self.eps, self.weight, self.bias, silu, x2=x2, pad=pad)
+        layout a conv(..., padded=True) reads (c2d_groupnorm_pad); mom: x's moments from its producing
+        conv (ops.GnMoments, c2d_groupnorm_moments), used when they match x and this norm's groups."""
+        return ops.group_norm(x, self.num_groups, self.eps, self.weight, self.bias, silu, x2=x2, pad=pad, mom=mom)
 
 
 class HLayerNorm(nn.Module):

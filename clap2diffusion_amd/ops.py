@@ -85,7 +85,7 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
          up: bool = False, x2: torch.Tensor | None = None, gn=None, gn_silu: bool = False, ln=None,
          silu_in: bool = False, act: str | None = None, temb: torch.Tensor | None = None,
          resid: torch.Tensor | None = None, out: torch.Tensor | None = None, padded: bool = False,
-         ln_fold=None) -> torch.Tensor:
+         ln_fold=None, gn_moments: int = 0):
     """Implicit-GEMM conv / linear (c2d::conv2d_igemm).
 
     x: NHWC [N, H, W, C0] fp16 (or 2-D [M, C0] for a linear layer); padded: x is the
@@ -93,6 +93,8 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
     gn: (scale, shift) fp32 [N, C0+C1]; ln: (stats [M, 2], gamma, beta).
     ln_fold: eps of a LayerNorm folded into this linear: x is the LayerNorm's raw input
     (weight = W diag(gamma), bias = b + W beta; fold_layernorm builds them), panel GEMM shapes only.
+    gn_moments = G > 0: also have the conv emit the GroupNorm moments of its output over G groups
+    where the library can (c2d_conv2d_gn_rows); returns (out, GnMoments or None) instead of out.
     """
     _require(x, "x")
     if x.dim() == 2:
@@ -121,9 +123,50 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
         assert resid.stride(-1) == 1
     gs, gh = gn if gn is not None else (None, None)
     ls, lg, lb = ln if ln is not None else (None, None, None)
+    mom, rows = None, 0
+    if gn_moments and x.dim() == 4 and x2 is None and act is None and not up and out.is_contiguous():
+        rows = gn_moment_rows(out.shape[0], oh, ow, x.shape[-1], cout, ksize, stride, bool(padded), resid is not None,
+                              temb is not None, gn_moments)
+        if rows:
+            mom = torch.empty((out.shape[0], oh * ow // rows, gn_moments, 2), device=x.device, dtype=torch.float32)
     C2D.conv2d_igemm(x, weight, kpad, cout, ksize, stride, up, x2, gs, gh, gn_silu, ls, lg, lb, silu_in, bias,
-                     C2D_ACT[act], temb, resid, out, bool(padded), float(ln_fold or 0.0))
+                     C2D_ACT[act], temb, resid, out, bool(padded), float(ln_fold or 0.0), mom, int(gn_moments))
+    if gn_moments:
+        return out, (GnMoments(out, mom, rows, gn_moments) if mom is not None else None)
     return out
+
+
+class GnMoments:
+    """GroupNorm moments a conv emitted for its output (c2d_conv_desc::gn_mom): mom fp32
+    [N][H*W / rows][groups][2] of {mean, M2}; valid for `of` (that exact tensor) until it is written again."""
+
+    def __init__(self, of: torch.Tensor, mom: torch.Tensor, rows: int, groups: int):
+        self.of, self.mom, self.rows, self.groups = of, mom, rows, groups
+
+    def matches(self, x: torch.Tensor, groups: int) -> bool:
+        return (x is self.of and groups == self.groups and x.dim() == 4 and
+                tuple(self.mom.shape[:1]) == tuple(x.shape[:1]))
+
+
+@functools.lru_cache(maxsize=None)
+def gn_moment_rows(n: int, oh: int, ow: int, cin: int, cout: int, ksize: int, stride: int, padded: bool, resid: bool,
+                   temb: bool, groups: int) -> int:
+    """c2d_conv2d_gn_rows for a conv of these shapes as ops.conv issues it (16-B aligned operands, a workspace
+    for any split): rows per moment block, 0 = this conv cannot emit its output's GroupNorm moments."""
+    import ctypes
+    from ._lib import ConvDesc, lib
+    d = ConvDesc()
+    h, w = (oh, ow) if padded or ksize == 1 or stride == 1 else (oh * stride, ow * stride)
+    d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride, d.src_pad = cin, n, h, w, oh, ow, ksize, stride, int(padded)
+    d.cout, d.kpad, d.out_ld = cout, kpad_of(ksize * ksize * cin), cout
+    d.out = 256
+    if resid:
+        d.resid, d.resid_ld = 256, cout
+    if temb:
+        d.temb, d.temb_ld = 256, cout
+    d.ws, d.ws_bytes = 256, 1 << 40
+    d.gn_groups = groups
+    return int(lib().c2d_conv2d_gn_rows(ctypes.byref(d)))
 
 
 @torch.no_grad()
@@ -217,12 +260,14 @@ class force_plan:
         self.prev = (t.value, sp.value)   # restored on exit: nested overrides / env sweeps survive
         check(lib().c2d_set_plan_override(self.tile, self.split), "c2d_set_plan_override")
         rowring_conv.cache_clear()        # the planner's answers change under an override
+        gn_moment_rows.cache_clear()
         return self
 
     def __exit__(self, *exc):
         from ._lib import lib
         lib().c2d_set_plan_override(*self.prev)
         rowring_conv.cache_clear()
+        gn_moment_rows.cache_clear()
         return False
 
 
@@ -259,12 +304,20 @@ def group_norm_apply(x: torch.Tensor, gn, silu: bool, x2: torch.Tensor | None = 
 
 
 def group_norm(x: torch.Tensor, groups: int, eps: float, gamma: torch.Tensor, beta: torch.Tensor, silu: bool,
-               x2: torch.Tensor | None = None, out: torch.Tensor | None = None, pad: bool = False) -> torch.Tensor:
+               x2: torch.Tensor | None = None, out: torch.Tensor | None = None, pad: bool = False,
+               mom: "GnMoments | None" = None) -> torch.Tensor:
     """act(GroupNorm(cat[x, x2])) in one c2d::groupnorm call (single fused kernel for
     small images, stats + apply otherwise).  pad: write the zero-bordered layout
-    [N, H + 2, W + 2, C] (c2d::groupnorm_pad) for a conv(..., padded=True)."""
+    [N, H + 2, W + 2, C] (c2d::groupnorm_pad) for a conv(..., padded=True).  mom: the moments x's
+    producing conv emitted (conv(..., gn_moments=groups)): one launch, no statistics pass."""
     _require(x, "x")
     c = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
+    if mom is not None and x2 is None and mom.matches(x, groups):
+        n, h, w, _ = x.shape
+        if out is None:
+            out = torch.empty((n, h + 2, w + 2, c) if pad else x.shape, device=x.device, dtype=F16)
+        C2D.groupnorm_moments(x, groups, float(eps), gamma, beta, bool(silu), mom.mom, mom.rows, bool(pad), out)
+        return out
     if pad:
         n, h, w, _ = x.shape
         if out is None:

@@ -24,7 +24,8 @@ _CU = "cuda"
 
 
 def _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma,
-               ln_beta, silu_in, bias, act, temb, resid, out, src_pad=False, lnf_eps=0.0) -> ConvDesc:
+               ln_beta, silu_in, bias, act, temb, resid, out, src_pad=False, lnf_eps=0.0, gn_mom=None,
+               gn_groups=0) -> ConvDesc:
     if x.dim() == 2:
         n, h, w = 1, 1, x.shape[0]
         c0 = x.shape[1]
@@ -62,6 +63,8 @@ def _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift,
     d.out = ptr(out)
     d.out_ld = out.stride(-2) if out.dim() == 2 else out.shape[-1]
     d.src_pad = int(src_pad)
+    if gn_mom is not None:
+        d.gn_mom = ptr(gn_mom); d.gn_groups = gn_groups
     return d
 
 
@@ -73,12 +76,15 @@ def conv2d_igemm(x: Tensor, weight: Tensor, kpad: int, cout: int, ksize: int, st
                  x2: Optional[Tensor], gn_scale: Optional[Tensor], gn_shift: Optional[Tensor], gn_silu: bool,
                  ln_stats: Optional[Tensor], ln_gamma: Optional[Tensor], ln_beta: Optional[Tensor], silu_in: bool,
                  bias: Optional[Tensor], act: int, temb: Optional[Tensor], resid: Optional[Tensor],
-                 out: Tensor, src_pad: bool = False, lnf_eps: float = 0.0) -> None:
+                 out: Tensor, src_pad: bool = False, lnf_eps: float = 0.0, gn_mom: Optional[Tensor] = None,
+                 gn_groups: int = 0) -> None:
     """c2d_conv2d_igemm (+ its split-K workspace, sized by c2d_conv2d_igemm_workspace_size).
     src_pad: x is the zero-bordered layout [n][h + 2][w + 2][c] (c2d_groupnorm_pad).
-    lnf_eps > 0: a LayerNorm (that eps) folded into the GEMM (C2D_PRO_LNFOLD)."""
+    lnf_eps > 0: a LayerNorm (that eps) folded into the GEMM (C2D_PRO_LNFOLD).
+    gn_mom: fp32 [n][hw / rows][gn_groups][2], the output's GroupNorm moments written by the conv
+    (c2d_conv_desc::gn_mom; rows = c2d_conv2d_gn_rows)."""
     d = _conv_desc(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma,
-                   ln_beta, silu_in, bias, act, temb, resid, out, src_pad, lnf_eps)
+                   ln_beta, silu_in, bias, act, temb, resid, out, src_pad, lnf_eps, gn_mom, gn_groups)
     wsb = lib().c2d_conv2d_igemm_workspace_size(ctypes.byref(d))
     if wsb:
         ws = torch.empty(wsb // 4, device=x.device, dtype=torch.float32)
@@ -92,7 +98,7 @@ def conv2d_igemm(x: Tensor, weight: Tensor, kpad: int, cout: int, ksize: int, st
 
 @conv2d_igemm.register_fake
 def _(x, weight, kpad, cout, ksize, stride, up, x2, gn_scale, gn_shift, gn_silu, ln_stats, ln_gamma, ln_beta,
-      silu_in, bias, act, temb, resid, out, src_pad=False, lnf_eps=0.0):
+      silu_in, bias, act, temb, resid, out, src_pad=False, lnf_eps=0.0, gn_mom=None, gn_groups=0):
     return None
 
 
@@ -143,6 +149,17 @@ def groupnorm_pad(x: Tensor, x2: Optional[Tensor], groups: int, eps: float, gamm
     ws = torch.empty((wsb + 15) // 16 * 4, device=x.device, dtype=torch.float32)
     check(lib().c2d_groupnorm_pad(ptr(x), ptr(x2), c0, c1, n, h, w, groups, eps, ptr(gamma), ptr(beta), int(silu),
                                   ptr(out), ptr(ws), wsb, stream_ptr()), "c2d_groupnorm_pad")
+
+
+@custom_op("c2d::groupnorm_moments", mutates_args=("out",), device_types=_CU)
+def groupnorm_moments(x: Tensor, groups: int, eps: float, gamma: Tensor, beta: Tensor, silu: bool, mom: Tensor,
+                      rows: int, pad: bool, out: Tensor) -> None:
+    """c2d_groupnorm_moments: x [n][h][w][c] normalised with the {mean, M2} moments its producing conv
+    wrote (mom [n][h*w / rows][groups][2]) -> out [n][h][w][c], or with pad the zero-bordered
+    [n][h + 2][w + 2][c]."""
+    n, h, w, c = x.shape
+    check(lib().c2d_groupnorm_moments(ptr(x), c, n, h * w, groups, eps, ptr(gamma), ptr(beta), int(silu), ptr(mom),
+                                      rows, w + 2 if pad else 0, ptr(out), stream_ptr()), "c2d_groupnorm_moments")
 
 
 @custom_op("c2d::layernorm_stats", mutates_args=("stats",), device_types=_CU)
@@ -259,12 +276,12 @@ def add(a: Tensor, b: Tensor, out: Tensor) -> None:
 
 
 # fake (meta) implementations: every op only mutates caller-allocated outputs
-for _op in (pack_weights, groupnorm_stats, groupnorm_apply, groupnorm, groupnorm_pad, layernorm_stats, layernorm, attention_fwd,
+for _op in (pack_weights, groupnorm_stats, groupnorm_apply, groupnorm, groupnorm_pad, groupnorm_moments, layernorm_stats, layernorm, attention_fwd,
             attention_small, window_attention, htsat_mel_patches, patch_merge_gather, row_mean, softmax_rows,
             l2_normalize, clap_log_mel, timestep_embedding, cfg_ddim_step, latent_to_nhwc, upsample_nearest2x, add):
     _op.register_fake(lambda *args, **kwargs: None)
 
-OPS = ("conv2d_igemm", "pack_weights", "groupnorm_stats", "groupnorm_apply", "groupnorm", "groupnorm_pad",
+OPS = ("conv2d_igemm", "pack_weights", "groupnorm_stats", "groupnorm_apply", "groupnorm", "groupnorm_pad", "groupnorm_moments",
        "layernorm_stats",
        "layernorm", "attention_fwd", "attention_small", "window_attention", "htsat_mel_patches", "patch_merge_gather",
        "row_mean", "softmax_rows", "l2_normalize", "clap_log_mel", "timestep_embedding", "cfg_ddim_step",

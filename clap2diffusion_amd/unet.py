@@ -57,6 +57,10 @@ FOLD_FF_OUT = os.environ.get("C2D_FOLD_FF_OUT", "1") != "0"
 # norm1 / norm3 folded into the QKV / GEGLU GEMMs where those run on the panel GEMM (K = 320):
 # A/B switch only (C2D_LN_FOLD=0 materialises the LayerNorm outputs)
 FOLD_LN = os.environ.get("C2D_LN_FOLD", "1") != "0"
+# GroupNorm moments from the producing conv (round 6, c2d_conv_desc::gn_mom): norm2 of every ResnetBlock2D and
+# the norm after a resnet read the statistics its row-ring conv emitted (one GroupNorm launch instead of two);
+# C2D_GN_MOMENTS=0 (A/B) keeps the statistics pass
+GN_MOMENTS = os.environ.get("C2D_GN_MOMENTS", "1") != "0"
 
 
 class Attention(nn.Module):
@@ -288,7 +292,7 @@ class Transformer2DModel(nn.Module):
         return out.view(b, x4.shape[1], x4.shape[2], c)
 
     def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None,
-                cfg_dup: torch.Tensor | None = None):
+                cfg_dup: torch.Tensor | None = None, x_mom=None):
         """cfg_dup: x is one half of a CFG pair with identical halves and the first half of this
         [2N, H, W, C] buffer; the output is the full pair (the block duplicates its state before
         the cross-attention, and x into the buffer's second half for proj_out's residual).  The
@@ -298,14 +302,14 @@ class Transformer2DModel(nn.Module):
         blk = self.transformer_blocks[0]
         fold = FOLD_FF_OUT and self.fold_ok
         if cfg_dup is None:
-            h = self.proj_in(self.norm.apply(x))
+            h = self.proj_in(self.norm.apply(x, mom=x_mom))
             if fold:
                 t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
                 return self._block_out(t, x, x)
             t = blk(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
             return self.proj_out(t.view(n, hh, ww, c), resid=x)
         hb = x.new_empty((2 * n, hh * ww, c))
-        h = self.proj_in(self.norm.apply(x), out=hb[:n].view(n, hh, ww, c))
+        h = self.proj_in(self.norm.apply(x, mom=x_mom), out=hb[:n].view(n, hh, ww, c))
         if fold:
             t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
                                  cfg_dup=hb)
@@ -329,7 +333,10 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = HConv2d(cin, cout, 1) if cin != cout else None
         self.temb_off = None  # column offset into the batched time_emb_proj output
 
-    def forward(self, x, temb_all=None, skip=None, out=None):
+    def forward(self, x, temb_all=None, skip=None, out=None, x_mom=None, want_mom: bool = False):
+        """x_mom: x's GroupNorm moments from its producer (ops.GnMoments) for norm1; want_mom: return
+        (out, moments of out for a following 32-group norm, or None).  conv1 emits norm2's moments
+        itself where the library can (the row-ring tiles: c2d_conv2d_gn_rows), so norm2 is one launch."""
         temb = None
         if temb_all is not None:
             temb = temb_all[:, self.temb_off:self.temb_off + self.cout]
@@ -338,10 +345,16 @@ class ResnetBlock2D(nn.Module):
         # act(GroupNorm) in the zero-bordered layout where the conv planner runs the row-ring 3x3
         # (tile 42: the c3 batch's level-0 convs), the plain layout elsewhere
         p1 = ops.rowring_conv(n, hh, ww, cin, self.cout)
-        h = self.conv1(self.norm1.apply(x, skip, silu=True, pad=p1), temb=temb, padded=p1)
+        a1 = self.norm1.apply(x, skip, silu=True, pad=p1, mom=x_mom if skip is None else None)
+        if GN_MOMENTS:
+            h, hm = self.conv1(a1, temb=temb, padded=p1, gn_moments=self.norm2.num_groups)
+        else:
+            h, hm = self.conv1(a1, temb=temb, padded=p1), None
         res = self.conv_shortcut(x, x2=skip) if self.conv_shortcut is not None else x
         p2 = ops.rowring_conv(n, hh, ww, self.cout, self.cout)
-        return self.conv2(self.norm2.apply(h, silu=True, pad=p2), resid=res, out=out, padded=p2)
+        y = self.conv2(self.norm2.apply(h, silu=True, pad=p2, mom=hm), resid=res, out=out, padded=p2,
+                       gn_moments=self.norm2.num_groups if want_mom and GN_MOMENTS else 0)
+        return (y, None) if want_mom and not GN_MOMENTS else y
 
 
 class Downsample2D(nn.Module):
@@ -535,16 +548,18 @@ class UNet2DConditionModel(nn.Module):
         else:
             h = self.conv_in(x)
             skips = [h]
+        # hm: GroupNorm moments of h from the conv that produced it (ops.GnMoments, or None), for the
+        # next norm over h (a transformer's norm, the next resnet's norm1); anything else drops them
         for i, blk in enumerate(self.down_blocks):
             for j, r in enumerate(blk.resnets):
                 pre = shared and i == 0 and j == 0   # still on one half of the CFG pair
                 if pre:   # the resnet output lands in the first half of its CFG-pair buffer
                     hb = h.new_empty((2 * h.shape[0], h.shape[1], h.shape[2], r.cout))
-                    h = r(h, temb_all, out=hb[:h.shape[0]])
+                    h, hm = r(h, temb_all, out=hb[:h.shape[0]], want_mom=True)
                 else:
-                    h = r(h, temb_all)
+                    h, hm = r(h, temb_all, want_mom=True)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw, em, cfg_dup=hb if pre else None)
+                    h = blk.attentions[j](h, ehs, kw, em, cfg_dup=hb if pre else None, x_mom=hm)
                 elif pre:
                     hb[h.shape[0]:].copy_(h)
                     h = hb
@@ -553,14 +568,14 @@ class UNet2DConditionModel(nn.Module):
                 h = blk.downsamplers[0](h)
                 skips.append(h)
         mb = self.mid_block
-        h = mb.resnets[0](h, temb_all)
-        h = mb.attentions[0](h, ehs, kw, em)
+        h, hm = mb.resnets[0](h, temb_all, want_mom=True)
+        h = mb.attentions[0](h, ehs, kw, em, x_mom=hm)
         h = mb.resnets[1](h, temb_all)
         for blk in self.up_blocks:
             for j, r in enumerate(blk.resnets):
-                h = r(h, temb_all, skip=skips.pop())
+                h, hm = r(h, temb_all, skip=skips.pop(), want_mom=True)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw, em)
+                    h = blk.attentions[j](h, ehs, kw, em, x_mom=hm)
             if hasattr(blk, "upsamplers"):
                 h = blk.upsamplers[0](h)
         return self.conv_out(self.conv_norm_out.apply(h, silu=True))

@@ -108,6 +108,16 @@ typedef struct c2d_conv_desc {
                                 border is read as data, so a GN / LN / SiLU would turn it into
                                 act(shift) instead of the zero padding torch applies        */
     float pro_eps;           /* C2D_PRO_LNFOLD: the LayerNorm eps                         */
+    /* r6: GroupNorm moments of the output, emitted by the producer (NULL = none).  When set,
+       the conv also writes, for every block of c2d_conv2d_gn_rows(d) output rows of one image
+       and every one of gn_groups channel groups, the fp32 pair {mean, M2} (M2 = sum of squared
+       deviations from that mean) of the fp16 values it stores: layout
+       [n][oh * ow / rows][gn_groups][2].  c2d_groupnorm_moments then normalises the output
+       without re-reading it for statistics.  Only where c2d_conv2d_gn_rows(d) > 0, else
+       C2D_E_SHAPE.  Callers built against the r5 header (no such fields) must not be mixed with
+       this library: the descriptor grew (c2d_version "r6").                              */
+    void* gn_mom;
+    int gn_groups;           /* channel groups of the moments (cout % gn_groups == 0)     */
 } c2d_conv_desc;
 
 int c2d_conv2d_igemm(const c2d_conv_desc* d, void* stream);
@@ -140,6 +150,19 @@ size_t c2d_conv2d_igemm_workspace_size(const c2d_conv_desc* d);
  * forces a plan (tuning and tests only).
  */
 int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit);
+
+/*
+ * Rows per GroupNorm-moment block if c2d_conv2d_igemm can emit the moments of this descriptor's
+ * output (c2d_conv_desc::gn_mom, gn_groups), 0 if not.  One-slice plans: the row-ring 3x3 tiles
+ * (42: 256 rows, 43 / 44: 128) and the 256 x 320 ping-pong tile 40 (256) with a residual or a time
+ * embedding (their workgroup-image epilogue computes each column's shifted moments over the tile from
+ * the stored fp16 values and folds them per group in a fixed order); split-K plans: the combine kernel
+ * (32-row blocks, exact per-thread moments merged in a fixed order).  Always act none, no
+ * quantisation-tail split, 16-B aligned outputs, 320 % (cout / gn_groups) == 0 and cout % 320 == 0.
+ * The SD1.5 UNet's ResnetBlock2D conv1 (+ temb) -> norm2, conv2 (+ residual) -> the next norm, and the
+ * Transformer2DModel output / downsampler -> the next resnet's norm1.
+ */
+int c2d_conv2d_gn_rows(const c2d_conv_desc* d);
 
 /*
  * Test / tuning hook: force the LDS-DMA tile configuration (tile_id, one of the ids
@@ -211,6 +234,18 @@ size_t c2d_groupnorm_pad_workspace_size(int n, int c, int h, int w);
 int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int c1, int n, int h, int w, int groups,
                       float eps, const float* gamma, const float* beta, int silu, void* out, void* ws,
                       size_t ws_bytes, void* stream);
+
+/*
+ * act(GroupNorm(src)) from moments its producer emitted (c2d_conv_desc::gn_mom): mom holds fp32
+ * {mean, M2} per (image, block of `rows` pixels, group), [n][hw / rows][groups][2].  Every apply
+ * workgroup of image n merges its image's blocks per group (Chan's pairwise update in fp64, fixed
+ * order: deterministic) and applies; one launch, no statistics pass over src.  pw = 0: plain output
+ * [n][hw][c]; pw = w + 2 (h = hw / w): the zero-bordered layout of c2d_groupnorm_pad.  One source
+ * (c <= 4096, multiple of 8), groups <= 256, hw % rows == 0.
+ */
+int c2d_groupnorm_moments(const void* src, int c, int n, int hw, int groups, float eps, const float* gamma,
+                          const float* beta, int silu, const float* mom, int rows, int pw, void* out,
+                          void* stream);
 
 /*
  * LayerNorm over rows of a row-major fp16 [m][c] matrix (leading dim ld).

@@ -20,7 +20,7 @@ static int fails = 0;
         }                                                                     \
     } while (0)
 
-static const int kTiles[] = {0, 1, 2, 3, 7, 8, 9, 25, 28, 29, 40, 41, 42, 43, 44, 50, 70};
+static const int kTiles[] = {0, 1, 2, 3, 7, 8, 9, 25, 28, 29, 40, 41, 42, 43, 44, 50, 70, 80, 81};
 
 static c2d_conv_desc desc(int n, int h, int w, int c0, int c1, int ksize, int stride, int cout, int act) {
     static char dummy[64] __attribute__((aligned(16)));

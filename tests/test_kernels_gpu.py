@@ -144,7 +144,7 @@ def test_conv3x3_split_k_epilogue(dev, n, h, c0, c1, cout, act):
 
 # every tile configuration left in igemm.hip's kDmaTiles, forced through
 # c2d_set_plan_override and confirmed through c2d_conv2d_igemm_plan
-DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3, 8, 9]
+DMA_TILE_IDS = [25, 40, 41, 28, 29, 7, 1, 2, 3, 8, 9, 80, 81]
 
 
 @pytest.mark.parametrize("tile", DMA_TILE_IDS)
@@ -371,7 +371,7 @@ def test_epilogue_operand_forms(dev, force_plan, tile, cout, temb, resid, bias):
     close(nchw(out), ref)
 
 
-@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 8, 9, 40)])   # odd column tiles: no GEGLU
+@pytest.mark.parametrize("tile", [t for t in DMA_TILE_IDS if t not in (7, 8, 9, 40, 80, 81)])   # odd column tiles: no GEGLU
 def test_every_dma_tile_forced_geglu(dev, force_plan, tile):
     m, cin, inner = 1024, 320, 640
     force_plan(tile, 1)
@@ -1101,3 +1101,79 @@ def test_pack_weights_matches_host_packer(dev, cout, cin, k, cin_pad):
     ref, kp_ref = (ops.pack_conv_weight(w, cin_pad=cin_pad) if k == 3 else ops.pack_linear_weight(w))
     out, kp = ops.pack_weights_device(w.to(dev), cin_pad=cin_pad)
     assert kp == kp_ref and torch.equal(out.cpu(), ref)
+
+
+# producer-emitted GroupNorm moments (c2d_conv_desc::gn_mom, round 6): the row-ring conv's epilogue
+# (one slice) or the split-K combine (splitk_reduce_gn_kernel) writes {mean, M2} per (image, row block,
+# group) of the fp16 values it stores; c2d_groupnorm_moments normalises from them.  Against torch fp32
+# GroupNorm of the stored conv output and against the statistics pass (c2d_groupnorm) on the same
+# tensor; |mean| >> std via a large bias.
+@pytest.mark.parametrize("tile,split,n,h,cin,cout,temb,mean,pad,silu", [
+    (42, 1, 2, 64, 320, 320, False, 0.0, True, True),     # L0 conv2 (+ residual) -> padded norm (tile 42, 256 rows)
+    (42, 1, 2, 64, 320, 320, True, 40.0, False, False),   # + time embedding, |mean| >> std
+    (43, 1, 4, 32, 320, 640, True, 0.0, True, True),      # L1 conv1 (tile 43, 128 rows, 20 channels per group)
+    (43, 1, 2, 32, 640, 640, False, -25.0, False, True),
+    (42, 5, 2, 64, 640, 320, True, 0.0, True, True),      # c2's L0 up conv: row ring, 5 slices -> the combine emits
+    (7, 4, 2, 64, 320, 320, False, 30.0, True, True),     # c2's L0 conv: 128 x 320 DMA tile, 4 slices
+    (43, 5, 2, 32, 640, 640, True, 0.0, False, True),     # c2's L1 conv: row ring, 5 slices
+    (40, 1, 2, 64, 320, 320, False, 20.0, True, True),    # the 256 x 320 ping-pong tile's workgroup epilogue
+])
+def test_conv_gn_moments(dev, force_plan, tile, split, n, h, cin, cout, temb, mean, pad, silu):
+    force_plan(tile, split)
+    groups, eps = 32, 1e-5
+    x = gen(n, cin, h, h, seed=301)
+    w = gen(cout, cin, 3, 3, seed=302, scale=1.0 / math.sqrt(9 * cin))
+    b = gen(cout, seed=303) + mean
+    r = gen(n, cout, h, h, seed=304)
+    te = gen(n, cout, seed=305) if temb else None
+    gamma, beta = gen(cout, seed=306).abs() + 0.5, gen(cout, seed=307)
+    wp, kp = ops.pack_conv_weight(w)
+    xp = F.pad(nhwc(x), (0, 0, 1, 1, 1, 1)).half().to(dev)   # zero-bordered source
+    with ops.record_conv_plans() as plans:
+        y, mom = ops.conv(xp, wp.to(dev), kp, cout, ksize=3, bias=b.float().to(dev), padded=True,
+                          temb=te.half().to(dev) if temb else None, resid=None if temb else nhwc(r).half().to(dev),
+                          gn_moments=groups)
+    rows = 32 if split > 1 else (256 if tile in (40, 42) else 128)
+    assert plans == [(tile, split)] and mom is not None and mom.rows == rows, (plans, mom and mom.rows)
+    g, bt = gamma.float().to(dev), beta.float().to(dev)
+    got = ops.group_norm(y, groups, eps, g, bt, silu, pad=pad, mom=mom)
+    ref_stats = ops.group_norm(y, groups, eps, g, bt, silu, pad=pad)   # the statistics pass on the same tensor
+    ref = F.group_norm(nchw(y.float().cpu()), groups, gamma, beta, eps)
+    if silu:
+        ref = F.silu(ref)
+    ref = nhwc(ref)
+    if pad:
+        assert got.shape == (n, h + 2, h + 2, cout) and got[:, 0].abs().max() == 0 and got[:, :, -1].abs().max() == 0
+        got, ref_stats = got[:, 1:-1, 1:-1], ref_stats[:, 1:-1, 1:-1]
+    close(got, ref, tol_max=1e-2, tol_l2=2e-3)
+    close(got, ref_stats, tol_max=1e-2, tol_l2=2e-3)
+    # the emitted moments themselves: per (image, group) mean / variance against fp64 over the stored output
+    yg = y.double().cpu().reshape(n, h * h, groups, cout // groups)
+    m_ref = yg.mean(dim=(1, 3))
+    v_ref = yg.var(dim=(1, 3), unbiased=False)
+    mm = mom.mom.double().cpu()   # [n][blocks][groups][2]
+    cnt = mom.rows * (cout // groups)
+    m_all = mm[..., 0].mean(1)
+    m2 = mm[..., 1].sum(1) + cnt * ((mm[..., 0] - m_all[:, None]) ** 2).sum(1)
+    v_all = m2 / (cnt * mm.shape[1])
+    assert torch.allclose(m_all, m_ref, rtol=1e-5, atol=1e-4 * v_ref.sqrt().max().item())
+    assert torch.allclose(v_all, v_ref, rtol=2e-3)
+
+
+def test_conv_gn_moments_refused_where_not_emitted(dev):
+    """A conv whose epilogue cannot emit moments (no residual / time embedding: the per-wave image
+    epilogue) returns none; the C entry refuses a descriptor asking for them (C2D_E_SHAPE) rather than
+    leaving them unwritten."""
+    import ctypes
+    from clap2diffusion_amd import torch_ops
+    from clap2diffusion_amd._lib import lib
+    x = torch.randn(16, 64, 64, 320, device=dev, dtype=torch.float16)
+    wp = torch.randn(320, 2880, device=dev, dtype=torch.float16) * 0.02
+    y, mom = ops.conv(x, wp, 2880, 320, ksize=3, gn_moments=32)
+    assert mom is None
+    out = torch.empty_like(x)
+    mbuf = torch.empty(16 * 16 * 32 * 2, device=dev)
+    d = torch_ops._conv_desc(x, wp, 2880, 320, 3, 1, False, None, None, None, False, None, None, None, False, None, 0,
+                             None, None, out, False, 0.0, mbuf, 32)
+    assert lib().c2d_conv2d_gn_rows(ctypes.byref(d)) == 0
+    assert lib().c2d_conv2d_igemm(ctypes.byref(d), None) == -2

@@ -27,15 +27,15 @@ def _plan(cin, cout, n, h, k, ws=True, geglu=False, c1=0):
     (320, 320, 2, 64, 3, False, (7, 4)),        # c2: L0 resnet conv
     (640, 640, 2, 32, 3, False, (7, 8)),        # c2: L1 resnet conv
     (2560, 1280, 2, 16, 3, False, (41, 16)),    # c2: L2 up-block conv (split 16)
-    (1280, 1280, 2, 8, 3, False, (3, 12)),      # c2: L3 resnet conv (split 12)
+    (1280, 1280, 2, 8, 3, False, (81, 12)),     # c2: L3 resnet conv (two K groups, split 12)
     (1280, 1280, 2, 16, 1, False, (3, 1)),      # c2: L2 projections
     (640, 5120, 2, 32, 1, True, (50, 1)),       # c2: L1 GEGLU (persistent tile)
     (320, 320, 8, 96, 1, False, (7, 1)),        # c5: L0 projections
     (640, 640, 8, 48, 3, False, (41, 1)),       # c5: L1 resnet conv
-    (1280, 1280, 16, 16, 1, False, (8, 1)),     # c3: L2 projections (128 x 160, two per CU)
+    (1280, 1280, 16, 16, 1, False, (80, 1)),    # c3: L2 projections (128 x 160, two K groups)
     (1280, 1280, 16, 8, 1, False, (3, 1)),      # c3: mid-block projections
     (256, 128, 8, 512, 1, False, (1, 1)),       # VAE decoder 512^2 shortcut
-    (6400, 1280, 16, 16, 1, False, (7, 2)),     # c3: L2 ff.net.2 + proj_out fold (K = 5C)
+    (6400, 1280, 16, 16, 1, False, (80, 1)),    # c3: L2 ff.net.2 + proj_out fold (K = 5C)
     (3200, 640, 8, 48, 1, False, (41, 1)),      # c5: L1 fold
     (6400, 1280, 2, 8, 1, False, (3, 12)),      # c2: L3 fold
 ])
@@ -80,3 +80,21 @@ def test_quantisation_tail_split_k_workspace(c0, c1):
     assert _plan(c0, 320, 8, 96, 3, c1=c1) == (40, 1)
     assert _plan(c0, 320, 1, 96, 3, c1=c1) == (7, 3)
     assert _ws(c0, 320, 8, 96, 3, c1=c1) == 3 * 9216 * 320 * 4
+
+
+@pytest.mark.parametrize("n,h,cin,cout,resid,temb,groups,want", [
+    (16, 64, 320, 320, True, False, 32, 256),    # c3 L0 conv2 (+ residual) on tile 42: 256-row blocks
+    (16, 64, 320, 320, False, True, 32, 256),    # c3 L0 conv1 (+ temb)
+    (16, 32, 640, 640, True, False, 32, 128),    # c3 L1 on tile 43: 128-row blocks
+    (16, 64, 320, 320, False, False, 32, 0),     # no residual / temb: the per-wave epilogue emits none
+    (16, 64, 320, 320, True, False, 30, 0),      # 320 / 30 groups do not tile the 320-column block
+    (2, 64, 320, 320, True, False, 32, 32),      # c2 L0: (7, 4) split K -> the combine emits, 32-row blocks
+    (2, 64, 640, 320, True, False, 32, 32),      # c2 L0 up conv: the row ring with split K (42, 5)
+    (2, 8, 1280, 1280, True, False, 32, 32),     # c2 L3 (81, 12): 8 x 8 = 64 pixels per image, two 32-row blocks
+    (2, 8, 1280, 1280, True, False, 128, 32),    # 128 groups of 10 channels tile the block too
+])
+def test_gn_moment_rows(n, h, cin, cout, resid, temb, groups, want):
+    """c2d_conv2d_gn_rows: which convs can emit their output's GroupNorm moments (c2d_conv_desc::gn_mom)
+    -- the one-slice row-ring plans with the workgroup-image epilogue -- as ops.gn_moment_rows asks it."""
+    from clap2diffusion_amd import ops
+    assert ops.gn_moment_rows(n, h, h, cin, cout, 3, 1, True, resid, temb, groups) == want
