@@ -20,6 +20,10 @@ namespace c2d {
 #define ATTN_WPE 4
 #endif
 
+#ifndef C2D_TUNE_ATTN_BUFLD
+#define C2D_TUNE_ATTN_BUFLD 1   // whole key tiles staged by buffer loads off a per-tile SGPR base (round 6); 0 = A/B builds
+#endif
+
 #ifndef C2D_TUNE_ATTN80
 #define C2D_TUNE_ATTN80 1   // d = 80: 1 = the PV row-sum column (round 6), 0 = VALU row sums (round 5; A/B builds)
 #endif
@@ -153,7 +157,33 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     const f16* kbase = k + (size_t)bk * lk * ldk + h * D;
     const f16* vbase = v + (size_t)bk * lk * ldv + h * D;
     f16x8 rk[NLD], rv[NLD];
+    // BUFLD (whole key tiles, lk % 64 == 0): the tile's K / V rows through buffer loads whose base is the
+    // tile's first row (SGPRs, advanced by SALU per tile) and whose per-lane offsets are loop-invariant,
+    // so staging a tile costs no 64-bit address VALU (7 of the d = 40 loop's VALU per wave-tile)
+    constexpr bool BUFLD = !MASK && C2D_TUNE_ATTN_BUFLD;
+    unsigned koff[NLD], voff[NLD];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+        const int idx = tid + NT * i, row = idx / C::DCH, ch = idx - row * C::DCH;
+        koff[i] = (unsigned)(2 * (row * ldk + ch * 8));
+        voff[i] = (unsigned)(2 * (row * ldv + ch * 8));
+    }
+    const char* ukb = uniform_ptr(kbase);
+    const char* uvb = uniform_ptr(vbase);
     auto gload = [&](int t) {
+        if constexpr (BUFLD) {
+            const __amdgpu_buffer_rsrc_t rks = make_rsrc(ukb + (size_t)t * 128 * ldk, (unsigned)(128 * ldk));
+            const __amdgpu_buffer_rsrc_t rvs = make_rsrc(uvb + (size_t)t * 128 * ldv, (unsigned)(128 * ldv));
+#pragma unroll
+            for (int i = 0; i < NLD; ++i) {
+                const int idx = tid + NT * i;
+                if (NT * i < 64 * C::DCH - (NT - 1) || idx < 64 * C::DCH) {
+                    rk[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rks, koff[i], 0, 0));
+                    rv[i] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rvs, voff[i], 0, 0));
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < NLD; ++i) {
             const int idx = tid + NT * i;

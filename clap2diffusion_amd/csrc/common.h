@@ -219,6 +219,11 @@ __device__ __forceinline__ const char* uniform_ptr(const void* p) {
     return (const char*)(((uint64_t)hi << 32) | lo);
 }
 
+// buffer resource over [base, base + bytes): loads / DMA pieces past num_records read zeros
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -425,9 +425,6 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 #undef C2D_WAITVM
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
 
 // one 1-KiB DMA piece: lane l's 16 bytes at rsrc.base + off land at lds + 16 l
 __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t r, char* lds, unsigned off) {
@@ -757,77 +754,74 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(IgemmParams p) {
 }
 
 // Split-K combine that also emits the output's GroupNorm moments (IgemmParams::gn_mom): block = kGnRb rows x
-// 320 columns of one image, 320 threads; thread t owns columns 4 (t % 80) .. +3 and rows t / 80, + 4, ...
-// (kGnRb / 4 of them).  Each output goes through splitk_reduce_kernel's arithmetic; the thread keeps its
-// fp16-rounded values and forms their exact (mean, M2) per column (two passes in registers), the four row
-// threads of a column merge in LDS (Chan, equal counts, fixed order), then each group's columns.  Writes
-// {mean, M2} per (image, kGnRb-row block, group): the layout c2d_groupnorm_moments reads.
-constexpr int kGnRb = 32;
+// 320 columns of one image, 640 threads; thread t owns columns 4 (t % 80) .. +3 of rows t / 80 and t / 80 + 8,
+// every slab load of both issued before the first add (as splitk_reduce_kernel's one quad per thread: the
+// combine stays a single round of HBM / L2 latency).  Each output goes through splitk_reduce_kernel's
+// arithmetic; the thread forms the exact (mean, M2) of its two fp16-rounded values per column, the eight
+// row threads of a column merge in LDS (Chan, equal counts, fixed order), then each group's columns.
+// Writes {mean, M2} per (image, kGnRb-row block, group): the layout c2d_groupnorm_moments reads.
+constexpr int kGnRb = 16;
 template <int KS, bool S16>
-__global__ void __launch_bounds__(320) splitk_reduce_gn_kernel(IgemmParams p) {
-    constexpr int RPT = kGnRb / 4;
-    __shared__ float2 cm[4][320];
+__global__ void __launch_bounds__(640) splitk_reduce_gn_kernel(IgemmParams p) {
+    __shared__ float2 cm[8][320];
     const int t = threadIdx.x, q = t % 80, rs = t / 80;
     const int m0 = blockIdx.x * kGnRb, j = blockIdx.y * 320 + 4 * q;
     const int hw = p.oh * p.ow;
     const size_t slab = (size_t)p.M * p.cout;
     float4 bv = {0.f, 0.f, 0.f, 0.f};
-    f16x4 tv = {0, 0, 0, 0};
+    f16x4 tv = {0, 0, 0, 0}, rv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
     if (p.bias) bv = *reinterpret_cast<const float4*>(p.bias + j);
     if (p.temb) tv = *reinterpret_cast<const f16x4*>(p.temb + (size_t)(m0 / hw) * p.temb_ld + j);
-    float y[RPT][4];
+    f32x4 v[2][KS];
 #pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-        const int m = m0 + rs + 4 * i;
-        const size_t src = (size_t)m * p.cout + j;
-        f32x4 v[KS];
+    for (int i = 0; i < 2; ++i) {
+        const int m = m0 + rs + 8 * i;
+        if (p.resid) rv[i] = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
 #pragma unroll
-        for (int sl = 0; sl < KS; ++sl) v[sl] = slab_quad<S16>(p.ws, src + sl * slab);
-        f32x4 acc = v[0];
+        for (int sl = 0; sl < KS; ++sl) v[i][sl] = slab_quad<S16>(p.ws, (size_t)m * p.cout + j + sl * slab);
+    }
+    float y[2][4];
+    const float b4[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-        for (int sl = 1; sl < KS; ++sl) acc += v[sl];
-        f16x4 rv = {0, 0, 0, 0};
-        if (p.resid) rv = *reinterpret_cast<const f16x4*>(p.resid + (size_t)m * p.resid_ld + j);
+    for (int i = 0; i < 2; ++i) {
+        f32x4 acc = v[i][0];
+#pragma unroll
+        for (int sl = 1; sl < KS; ++sl) acc += v[i][sl];
         f16x4 o;
-        const float b4[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             float x = acc[r] + b4[r];
             if (p.temb) x += (float)tv[r];
-            if (p.resid) x += (float)rv[r];
+            if (p.resid) x += (float)rv[i][r];
             o[r] = (f16)x;
             y[i][r] = (float)o[r];
         }
-        *reinterpret_cast<f16x4*>(p.out + (size_t)m * p.out_ld + j) = o;
+        *reinterpret_cast<f16x4*>(p.out + (size_t)(m0 + rs + 8 * i) * p.out_ld + j) = o;
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 4; ++r) {   // two values: mean, M2 = (a - b)^2 / 2
+        const float d = y[0][r] - y[1][r];
+        cm[rs][4 * q + r] = make_float2(0.5f * (y[0][r] + y[1][r]), 0.5f * d * d);
+    }
+    __syncthreads();
+    float2 col = {0.f, 0.f};
+    if (t < 320) {   // per column t: merge the eight row threads (equal counts 2)
         float mu = 0.f;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) mu += y[i][r];
-        mu *= 1.0f / RPT;
+        for (int k = 0; k < 8; ++k) mu += cm[k][t].x;
+        mu *= 0.125f;
         float m2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < RPT; ++i) m2 = fmaf(y[i][r] - mu, y[i][r] - mu, m2);
-        cm[rs][4 * q + r] = make_float2(mu, m2);
+        for (int k = 0; k < 8; ++k) {
+            const float d = cm[k][t].x - mu;
+            m2 += cm[k][t].y + 2.0f * d * d;
+        }
+        col = make_float2(mu, m2);
     }
+    __syncthreads();
+    if (t < 320) cm[0][t] = col;
     __syncthreads();
     const int cpg = p.gn_cpg, ng = 320 / cpg;
-    {   // per column t: merge the four row threads (equal counts RPT)
-        float mu = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) mu += cm[k][t].x;
-        mu *= 0.25f;
-        float m2 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float d = cm[k][t].x - mu;
-            m2 += cm[k][t].y + (float)RPT * d * d;
-        }
-        __syncthreads();
-        cm[0][t] = make_float2(mu, m2);
-    }
-    __syncthreads();
     if (t < ng) {   // per group: its columns (equal counts kGnRb)
         float mg = 0.f;
         for (int i = 0; i < cpg; ++i) mg += cm[0][t * cpg + i].x;
@@ -845,7 +839,7 @@ __global__ void __launch_bounds__(320) splitk_reduce_gn_kernel(IgemmParams p) {
 
 void run_splitk_reduce(const IgemmParams& p, hipStream_t s) {
     if (p.gn_mom) {   // gn_rows_for: cout % 320 == 0, hw % kGnRb == 0, act none
-        const dim3 grid((unsigned)(p.M / kGnRb), (unsigned)(p.cout / 320)), blk(320);
+        const dim3 grid((unsigned)(p.M / kGnRb), (unsigned)(p.cout / 320)), blk(640);
 #define C2D_SKG(KS)                                                                                    \
     if (p.slab16) hipLaunchKernelGGL((splitk_reduce_gn_kernel<KS, true>), grid, blk, 0, s, p);        \
     else hipLaunchKernelGGL((splitk_reduce_gn_kernel<KS, false>), grid, blk, 0, s, p)
@@ -1409,7 +1403,7 @@ static bool gn_split_ok(int ks) {   // the slice counts splitk_reduce_gn_kernel 
 static int gn_rows_for(const c2d_conv_desc* d) {
     if (!d || d->gn_groups <= 0 || d->cout % d->gn_groups) return 0;
     const int cpg = d->cout / d->gn_groups;
-    if (320 % cpg || d->cout % 320 || !(d->resid || d->temb) || d->act != C2D_ACT_NONE) return 0;
+    if (320 % cpg || d->cout % 320 || d->act != C2D_ACT_NONE) return 0;
     if ((d->out_ld & 7) || (d->resid && (d->resid_ld & 7)) || (d->temb && (d->temb_ld & 7)) || d->out_ld < d->cout) return 0;
     if (((uintptr_t)d->out | (uintptr_t)d->resid | (uintptr_t)d->temb) & 15) return 0;
     if (d->ksize < 1 || d->oh <= 0 || d->ow <= 0 || d->n <= 0 || d->kpad < 64 || !dma_eligible(d)) return 0;
@@ -1429,6 +1423,7 @@ static int gn_rows_for(const c2d_conv_desc* d) {
         }
         return gn_split_ok(pl.split) && ((long)d->oh * d->ow) % kGnRb == 0 ? kGnRb : 0;
     }
+    if (!(d->resid || d->temb)) return 0;   // one slice: only the workgroup-image epilogue emits them
     if (pl.id == 40) return ((long)d->oh * d->ow) % 256 == 0 ? 256 : 0;   // ping-pong 256 x 320 (igemm_pp16.h)
     if (pl.id != 42 && pl.id != 43 && pl.id != 44) return 0;
     return pl.id == 42 ? 256 : 128;

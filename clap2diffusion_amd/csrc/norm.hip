@@ -331,9 +331,10 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const f16* __restrict__ s
 // an image: the fold order does not depend on the workgroup.
 //
 // MOM: ws holds {mean, M2} per (image, block of mrows pixels, group) written by the producing conv
-// (c2d_conv_desc::gn_mom) instead of shifted sums: each of the `parts` threads of a group merges
-// every parts-th block (Chan's pairwise update, equal counts, fp64), then the group's thread merges
-// the parts in order.  Deterministic; no pass over the source for statistics.
+// (c2d_conv_desc::gn_mom) instead of shifted sums: each of the `parts` threads of a group sums every
+// parts-th block's shifted mean, its square and its M2 (fp64), then the group's thread adds the parts in
+// order and forms the group's mean and M2 (equal block counts: no per-block divisions).  Deterministic;
+// no pass over the source for statistics.
 template <int CPT, bool PAD, bool MOM = false>
 __global__ void __launch_bounds__(256) gn_apply_fold_kernel(const f16* __restrict__ s0, const f16* __restrict__ s1,
                                                             int c0, int c1, int hw, int cpg, int nblk, float eps,
@@ -350,37 +351,40 @@ __global__ void __launch_bounds__(256) gn_apply_fold_kernel(const f16* __restric
     const size_t img = (size_t)n * hw;
     const int parts = 256 / groups;
     if constexpr (MOM) {
-        const double nb = (double)mrows * cpg;   // values per block and group
+        // equal counts nb per block: mean = s + S1 / K, M2 = Q + nb (S2 - S1^2 / K) with S1, S2 the sums of
+        // (mean_k - s), (mean_k - s)^2 over the K blocks and Q the sum of their M2; s = block 0's mean
+        // (the blocks' means sit close together, so the shifted sums stay well conditioned in fp64)
+        const double nb = (double)mrows * cpg;
         if (t < parts * groups) {
             const int g = t % groups, pt = t / groups;
             const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * groups + g;
-            double na = 0.0, ma = 0.0, qa = 0.0;
+            const double sh = (double)wp[0].x;
+            double a = 0.0, b = 0.0, qq = 0.0;
             for (int k = pt; k < nblk; k += parts) {
                 const float2 v = wp[(size_t)k * groups];
-                const double nn = na + nb, d = (double)v.x - ma;
-                ma += d * (nb / nn);
-                qa += (double)v.y + d * d * (na * nb / nn);
-                na = nn;
+                const double d = (double)v.x - sh;
+                a += d;
+                b += d * d;
+                qq += (double)v.y;
             }
-            dacc[t * 3] = na;
-            dacc[t * 3 + 1] = ma;
-            dacc[t * 3 + 2] = qa;
+            dacc[t * 3] = a;
+            dacc[t * 3 + 1] = b;
+            dacc[t * 3 + 2] = qq;
         }
         __syncthreads();
         if (t < groups) {
-            double na = 0.0, ma = 0.0, qa = 0.0;
+            double a = 0.0, b = 0.0, qq = 0.0;
             for (int pt = 0; pt < parts; ++pt) {
                 const int u = (pt * groups + t) * 3;
-                const double nb2 = dacc[u];
-                if (nb2 == 0.0) continue;
-                const double nn = na + nb2, d = dacc[u + 1] - ma;
-                ma += d * (nb2 / nn);
-                qa += dacc[u + 2] + d * d * (na * nb2 / nn);
-                na = nn;
+                a += dacc[u];
+                b += dacc[u + 1];
+                qq += dacc[u + 2];
             }
-            double var = qa / na;
+            const float2* wp = reinterpret_cast<const float2*>(ws) + (size_t)n * nblk * groups + t;
+            const double K = (double)nblk;
+            double var = (qq + nb * (b - a * a / K)) / (K * nb);
             if (var < 0.0) var = 0.0;
-            gmr[t * 2] = (float)ma;
+            gmr[t * 2] = (float)((double)wp[0].x + a / K);
             gmr[t * 2 + 1] = (float)(1.0 / sqrt(var + (double)eps));
         }
     } else {

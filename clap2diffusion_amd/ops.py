@@ -124,9 +124,9 @@ def conv(x: torch.Tensor, weight: torch.Tensor, kpad: int, cout: int, *, ksize: 
     gs, gh = gn if gn is not None else (None, None)
     ls, lg, lb = ln if ln is not None else (None, None, None)
     mom, rows = None, 0
-    if gn_moments and x.dim() == 4 and x2 is None and act is None and not up and out.is_contiguous():
+    if gn_moments and x.dim() == 4 and act is None and not up and out.is_contiguous():
         rows = gn_moment_rows(out.shape[0], oh, ow, x.shape[-1], cout, ksize, stride, bool(padded), resid is not None,
-                              temb is not None, gn_moments)
+                              temb is not None, gn_moments, x2.shape[-1] if x2 is not None else 0)
         if rows:
             mom = torch.empty((out.shape[0], oh * ow // rows, gn_moments, 2), device=x.device, dtype=torch.float32)
     C2D.conv2d_igemm(x, weight, kpad, cout, ksize, stride, up, x2, gs, gh, gn_silu, ls, lg, lb, silu_in, bias,
@@ -150,7 +150,7 @@ class GnMoments:
 
 @functools.lru_cache(maxsize=None)
 def gn_moment_rows(n: int, oh: int, ow: int, cin: int, cout: int, ksize: int, stride: int, padded: bool, resid: bool,
-                   temb: bool, groups: int) -> int:
+                   temb: bool, groups: int, c1: int = 0) -> int:
     """c2d_conv2d_gn_rows for a conv of these shapes as ops.conv issues it (16-B aligned operands, a workspace
     for any split): rows per moment block, 0 = this conv cannot emit its output's GroupNorm moments."""
     import ctypes
@@ -158,7 +158,10 @@ def gn_moment_rows(n: int, oh: int, ow: int, cin: int, cout: int, ksize: int, st
     d = ConvDesc()
     h, w = (oh, ow) if padded or ksize == 1 or stride == 1 else (oh * stride, ow * stride)
     d.c0, d.n, d.h, d.w, d.oh, d.ow, d.ksize, d.stride, d.src_pad = cin, n, h, w, oh, ow, ksize, stride, int(padded)
-    d.cout, d.kpad, d.out_ld = cout, kpad_of(ksize * ksize * cin), cout
+    d.c1 = c1
+    if c1:
+        d.src1 = 256
+    d.cout, d.kpad, d.out_ld = cout, kpad_of(ksize * ksize * (cin + c1)), cout
     d.out = 256
     if resid:
         d.resid, d.resid_ld = 256, cout

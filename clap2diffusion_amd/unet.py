@@ -61,6 +61,11 @@ FOLD_LN = os.environ.get("C2D_LN_FOLD", "1") != "0"
 # the norm after a resnet read the statistics its row-ring conv emitted (one GroupNorm launch instead of two);
 # C2D_GN_MOMENTS=0 (A/B) keeps the statistics pass
 GN_MOMENTS = os.environ.get("C2D_GN_MOMENTS", "1") != "0"
+GN_GROUPS = 32   # every GroupNorm the moments feed (SD1.5 norm_num_groups)
+# the CFG-shared prefix (conv_in, the first resnet and self-attention once per latent) from this many latents
+# per call: A/B switch (at one latent every kernel is latency bound and the half-batch saves less than the
+# duplicating copies cost)
+CFG_PREFIX_MIN = int(os.environ.get("C2D_CFG_PREFIX_MIN", "1"))
 
 
 class Attention(nn.Module):
@@ -280,24 +285,36 @@ class Transformer2DModel(nn.Module):
         self.w_out_fold.copy_(torch.cat([wp, wp @ w2], 1).to(torch.float16))
         self.b_out_fold.copy_(wp @ ff2.bias.float() + self.proj_out.bias.float())
 
-    def _block_out(self, t: torch.Tensor, x4: torch.Tensor, resid: torch.Tensor) -> torch.Tensor:
+    def _block_out(self, t: torch.Tensor, x4: torch.Tensor, resid: torch.Tensor, gm: int = 0):
         """Feed-forward + proj_out (+ resid) of the attention-part output t [B, L, C]:
-        proj_out(t + ff(t)) + resid, as one K = 5C GEMM over [t; GEGLU(LN3(t))]."""
+        proj_out(t + ff(t)) + resid, as one K = 5C GEMM over [t; GEGLU(LN3(t))].  gm > 0: (out, the
+        GroupNorm moments over gm groups the GEMM emitted for the next norm, or None)."""
         blk = self.transformer_blocks[0]
         b, l, c = t.shape
+        hh, ww = x4.shape[1], x4.shape[2]
         t2 = t.view(b * l, c)
         ff1 = blk.ff_inner(t2)
-        out = ops.conv(t2, self.w_out_fold, self.fold_kpad, c, ksize=1, bias=self.b_out_fold, x2=ff1,
-                       resid=resid.reshape(b * l, c))
-        return out.view(b, x4.shape[1], x4.shape[2], c)
+        r = ops.conv(t2.view(b, hh, ww, c), self.w_out_fold, self.fold_kpad, c, ksize=1, bias=self.b_out_fold,
+                     x2=ff1.view(b, hh, ww, ff1.shape[-1]), resid=resid.reshape(b, hh, ww, c),
+                     gn_moments=gm)
+        return r
 
     def forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask=None,
-                cfg_dup: torch.Tensor | None = None, x_mom=None):
+                cfg_dup: torch.Tensor | None = None, x_mom=None, want_mom: bool = False):
         """cfg_dup: x is one half of a CFG pair with identical halves and the first half of this
         [2N, H, W, C] buffer; the output is the full pair (the block duplicates its state before
         the cross-attention, and x into the buffer's second half for proj_out's residual).  The
         duplicates are one device copy of a half each -- a torch.cat of the halves read 1 and
-        wrote 2 half-tensors (30 us per call at level 0)."""
+        wrote 2 half-tensors (30 us per call at level 0).  x_mom: x's GroupNorm moments from its
+        producer (ops.GnMoments) for self.norm; want_mom: return (out, the moments of out that its
+        GEMM emitted for the next norm, or None)."""
+        gm = GN_GROUPS if want_mom and GN_MOMENTS else 0
+        r = self._forward(x, ehs, cross_attention_kwargs, encoder_attention_mask, cfg_dup, x_mom, gm)
+        if want_mom and not gm:
+            return r, None
+        return r
+
+    def _forward(self, x, ehs, cross_attention_kwargs, encoder_attention_mask, cfg_dup, x_mom, gm):
         n, hh, ww, c = x.shape
         blk = self.transformer_blocks[0]
         fold = FOLD_FF_OUT and self.fold_ok
@@ -305,19 +322,19 @@ class Transformer2DModel(nn.Module):
             h = self.proj_in(self.norm.apply(x, mom=x_mom))
             if fold:
                 t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
-                return self._block_out(t, x, x)
+                return self._block_out(t, x, x, gm)
             t = blk(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask)
-            return self.proj_out(t.view(n, hh, ww, c), resid=x)
+            return self.proj_out(t.view(n, hh, ww, c), resid=x, gn_moments=gm)
         hb = x.new_empty((2 * n, hh * ww, c))
         h = self.proj_in(self.norm.apply(x, mom=x_mom), out=hb[:n].view(n, hh, ww, c))
         if fold:
             t = blk.forward_attn(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask,
                                  cfg_dup=hb)
             cfg_dup[n:].copy_(cfg_dup[:n])
-            return self._block_out(t, cfg_dup, cfg_dup)
+            return self._block_out(t, cfg_dup, cfg_dup, gm)
         t = blk(h.view(n, hh * ww, c), ehs, cross_attention_kwargs, encoder_attention_mask, cfg_dup=hb)
         cfg_dup[n:].copy_(cfg_dup[:n])
-        return self.proj_out(t.view(2 * n, hh, ww, c), resid=cfg_dup)
+        return self.proj_out(t.view(2 * n, hh, ww, c), resid=cfg_dup, gn_moments=gm)
 
 
 class ResnetBlock2D(nn.Module):
@@ -362,8 +379,11 @@ class Downsample2D(nn.Module):
         super().__init__()
         self.conv = HConv2d(c, c, 3, stride=2)
 
-    def forward(self, x):
-        return self.conv(x)
+    def forward(self, x, want_mom: bool = False):
+        """want_mom: (out, its GroupNorm moments for the next resnet's norm1, or None)."""
+        if want_mom and GN_MOMENTS:
+            return self.conv(x, gn_moments=GN_GROUPS)
+        return (self.conv(x), None) if want_mom else self.conv(x)
 
 
 class Upsample2D(nn.Module):
@@ -536,7 +556,7 @@ class UNet2DConditionModel(nn.Module):
         em = encoder_attention_mask
         if temb_all is None:
             temb_all = self.time_conditioning(t_sin)
-        shared = cfg_pair and self.cfg_shared_prefix_ok()
+        shared = cfg_pair and x.shape[0] >= CFG_PREFIX_MIN and self.cfg_shared_prefix_ok()
         if cfg_pair and not shared:
             x = torch.cat([x, x], 0)
         if shared:   # conv_in runs on one half, written into the first half of the skip buffer
@@ -550,35 +570,38 @@ class UNet2DConditionModel(nn.Module):
             skips = [h]
         # hm: GroupNorm moments of h from the conv that produced it (ops.GnMoments, or None), for the
         # next norm over h (a transformer's norm, the next resnet's norm1); anything else drops them
+        hm = None
         for i, blk in enumerate(self.down_blocks):
             for j, r in enumerate(blk.resnets):
                 pre = shared and i == 0 and j == 0   # still on one half of the CFG pair
                 if pre:   # the resnet output lands in the first half of its CFG-pair buffer
                     hb = h.new_empty((2 * h.shape[0], h.shape[1], h.shape[2], r.cout))
-                    h, hm = r(h, temb_all, out=hb[:h.shape[0]], want_mom=True)
+                    h, hm = r(h, temb_all, out=hb[:h.shape[0]], x_mom=hm, want_mom=True)
                 else:
-                    h, hm = r(h, temb_all, want_mom=True)
+                    h, hm = r(h, temb_all, x_mom=hm, want_mom=True)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw, em, cfg_dup=hb if pre else None, x_mom=hm)
+                    h, hm = blk.attentions[j](h, ehs, kw, em, cfg_dup=hb if pre else None, x_mom=hm, want_mom=True)
                 elif pre:
                     hb[h.shape[0]:].copy_(h)
-                    h = hb
+                    h, hm = hb, None
                 skips.append(h)
             if hasattr(blk, "downsamplers"):
-                h = blk.downsamplers[0](h)
+                h, hm = blk.downsamplers[0](h, want_mom=True)
                 skips.append(h)
         mb = self.mid_block
-        h, hm = mb.resnets[0](h, temb_all, want_mom=True)
-        h = mb.attentions[0](h, ehs, kw, em, x_mom=hm)
-        h = mb.resnets[1](h, temb_all)
+        h, hm = mb.resnets[0](h, temb_all, x_mom=hm, want_mom=True)
+        h, hm = mb.attentions[0](h, ehs, kw, em, x_mom=hm, want_mom=True)
+        h = mb.resnets[1](h, temb_all, x_mom=hm)
         for blk in self.up_blocks:
-            for j, r in enumerate(blk.resnets):
+            for j, r in enumerate(blk.resnets):   # norm1 over [h; skip]: no producer moments
                 h, hm = r(h, temb_all, skip=skips.pop(), want_mom=True)
                 if len(blk.attentions):
-                    h = blk.attentions[j](h, ehs, kw, em, x_mom=hm)
+                    h, hm = blk.attentions[j](h, ehs, kw, em, x_mom=hm, want_mom=True)
+                else:
+                    hm = None
             if hasattr(blk, "upsamplers"):
-                h = blk.upsamplers[0](h)
-        return self.conv_out(self.conv_norm_out.apply(h, silu=True))
+                h, hm = blk.upsamplers[0](h), None
+        return self.conv_out(self.conv_norm_out.apply(h, silu=True, mom=hm))
 
     def forward(self, sample: torch.Tensor, timestep, encoder_hidden_states: torch.Tensor,
                 cross_attention_kwargs: dict | None = None, return_dict: bool = True,

@@ -157,7 +157,7 @@ int c2d_conv2d_igemm_plan(const c2d_conv_desc* d, int* tile_id, int* ksplit);
  * (42: 256 rows, 43 / 44: 128) and the 256 x 320 ping-pong tile 40 (256) with a residual or a time
  * embedding (their workgroup-image epilogue computes each column's shifted moments over the tile from
  * the stored fp16 values and folds them per group in a fixed order); split-K plans: the combine kernel
- * (32-row blocks, exact per-thread moments merged in a fixed order).  Always act none, no
+ * (16-row blocks, exact per-thread moments merged in a fixed order).  Always act none, no
  * quantisation-tail split, 16-B aligned outputs, 320 % (cout / gn_groups) == 0 and cout % 320 == 0.
  * The SD1.5 UNet's ResnetBlock2D conv1 (+ temb) -> norm2, conv2 (+ residual) -> the next norm, and the
  * Transformer2DModel output / downsampler -> the next resnet's norm1.
@@ -238,8 +238,9 @@ int c2d_groupnorm_pad(const void* src0, const void* src1, int c0, int c1, int n,
 /*
  * act(GroupNorm(src)) from moments its producer emitted (c2d_conv_desc::gn_mom): mom holds fp32
  * {mean, M2} per (image, block of `rows` pixels, group), [n][hw / rows][groups][2].  Every apply
- * workgroup of image n merges its image's blocks per group (Chan's pairwise update in fp64, fixed
- * order: deterministic) and applies; one launch, no statistics pass over src.  pw = 0: plain output
+ * workgroup of image n merges its image's blocks per group (equal block counts: fp64 sums of the
+ * blocks' M2 and of their means shifted by block 0's, fixed order: deterministic) and applies; one
+ * launch, no statistics pass over src.  pw = 0: plain output
  * [n][hw][c]; pw = w + 2 (h = hw / w): the zero-bordered layout of c2d_groupnorm_pad.  One source
  * (c <= 4096, multiple of 8), groups <= 256, hw % rows == 0.
  */

@@ -8,6 +8,7 @@
 #   VARIANTS="base:C2D_LIB=clap2diffusion_amd/libc2d_hip.so gn0:C2D_LIB=clap2diffusion_amd/libc2d_hip_gn0.so"
 #   CMD=norm   each arm runs scripts/bench_norm_graph.py (graph-replayed GN / LN shapes)
 #   CMD=shapes each arm runs scripts/unet_shapes.py (per-shape GEMM breakdown)
+#   CMD=attn   each arm runs scripts/bench_attn.py (the UNet attention shapes, random operands)
 #   CMD=bench  (default) the bench line with BENCH_ARGS (default: short, no CPU / PMC / configs)
 # PYTEST_K (optional): run that -m gpu subset once per arm first.  Stops at the first failure.
 set -o pipefail
@@ -38,6 +39,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
     echo "== $label (round $r)"
     case ${CMD:-bench} in
       norm) arm "$label" "$envs" timeout -k 10 120 python -u scripts/bench_norm_graph.py 2>&1 | grep -E "^(GN|LN)" || exit 1 ;;
+      attn) arm "$label" "$envs" timeout -k 10 200 python -u scripts/bench_attn.py 2>&1 | grep -v "amdgpu.ids\|^\[W" || exit 1 ;;
       shapes) arm "$label" "$envs" timeout -k 10 300 python -u scripts/unet_shapes.py 2>&1 | grep -v "amdgpu.ids\|^\[W" \
                 | head -${SHAPES_LINES:-24} || exit 1 ;;
       bench) arm "$label" "$envs" timeout -k 10 400 python -u bench.py $BENCH_ARGS > gpurun_out/ab/${label}_$r.json \

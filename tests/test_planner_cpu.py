@@ -88,10 +88,10 @@ def test_quantisation_tail_split_k_workspace(c0, c1):
     (16, 32, 640, 640, True, False, 32, 128),    # c3 L1 on tile 43: 128-row blocks
     (16, 64, 320, 320, False, False, 32, 0),     # no residual / temb: the per-wave epilogue emits none
     (16, 64, 320, 320, True, False, 30, 0),      # 320 / 30 groups do not tile the 320-column block
-    (2, 64, 320, 320, True, False, 32, 32),      # c2 L0: (7, 4) split K -> the combine emits, 32-row blocks
-    (2, 64, 640, 320, True, False, 32, 32),      # c2 L0 up conv: the row ring with split K (42, 5)
-    (2, 8, 1280, 1280, True, False, 32, 32),     # c2 L3 (81, 12): 8 x 8 = 64 pixels per image, two 32-row blocks
-    (2, 8, 1280, 1280, True, False, 128, 32),    # 128 groups of 10 channels tile the block too
+    (2, 64, 320, 320, True, False, 32, 16),      # c2 L0: (7, 4) split K -> the combine emits, 16-row blocks
+    (2, 64, 640, 320, True, False, 32, 16),      # c2 L0 up conv: the row ring with split K (42, 5)
+    (2, 8, 1280, 1280, True, False, 32, 16),     # c2 L3 (81, 12): 8 x 8 = 64 pixels per image, four 16-row blocks
+    (2, 8, 1280, 1280, True, False, 128, 16),    # 128 groups of 10 channels tile the block too
 ])
 def test_gn_moment_rows(n, h, cin, cout, resid, temb, groups, want):
     """c2d_conv2d_gn_rows: which convs can emit their output's GroupNorm moments (c2d_conv_desc::gn_mom)
