@@ -71,7 +71,8 @@ def _work(name: str, a: dict, out) -> tuple[str, str, float, float]:
         desc = (f"{'3x3' if k == 3 else '1x1'} M={m} {cin}->{cout}" + (f" s{a['stride']}" if a["stride"] > 1 else "")
                 + (" up" if a["up"] else "") + (" pad" if a["padded"] else "") + (f" {act}" if act else "")
                 + (" +gn" if a["gn"] is not None else "") + (" +ln" if a["ln"] is not None else "")
-                + (" +res" if a["resid"] is not None else "") + (" +temb" if a["temb"] is not None else ""))
+                + (" +res" if a["resid"] is not None else "") + (" +temb" if a["temb"] is not None else "")
+                + (" +gnm" if a.get("gn_moments") else ""))
         return fam, desc, flop, byts
     if name == "attention":
         bh, lq, lk, d = a["batch"] * a["heads"], a["lq"], a["lk"], a["d"]
@@ -85,7 +86,7 @@ def _work(name: str, a: dict, out) -> tuple[str, str, float, float]:
         byts = _nb(x) + _nb(x2) + (_nb(out) if name != "group_norm_stats" else 0)
         flag = {"group_norm": " pad" if a.get("pad") else "", "group_norm_stats": " stats",
                 "group_norm_apply": " apply"}[name]
-        silu = " silu" if a.get("silu") else ""
+        silu = (" silu" if a.get("silu") else "") + (" mom" if a.get("mom") is not None else "")
         c = x.shape[-1] + (x2.shape[-1] if x2 is not None else 0)
         return "groupnorm", f"GN {tuple(x.shape[:-1])}x{c}{flag}{silu}", 0.0, float(byts)
     if name in ("layer_norm", "layer_norm_stats"):
@@ -112,11 +113,12 @@ class Recorder:
         sig = inspect.signature(fn)
 
         def rec(*args, **kw):
-            out = fn(*args, **kw)
+            res = fn(*args, **kw)
             b = sig.bind(*args, **kw)
             b.apply_defaults()
-            self.calls.append((name, b, out))
-            return out
+            # conv(..., gn_moments=G) returns (out, moments): the row accounts the output tensor
+            self.calls.append((name, b, res[0] if isinstance(res, tuple) else res))
+            return res
         return rec
 
     def __enter__(self):
