@@ -57,6 +57,7 @@ FOLD_FF_OUT = os.environ.get("C2D_FOLD_FF_OUT", "1") != "0"
 # norm1 / norm3 folded into the QKV / GEGLU GEMMs where those run on the panel GEMM (K = 320):
 # A/B switch only (C2D_LN_FOLD=0 materialises the LayerNorm outputs)
 FOLD_LN = os.environ.get("C2D_LN_FOLD", "1") != "0"
+FOLD_LN640 = os.environ.get("C2D_LN_FOLD640", "1") != "0"   # the K = 640 one-round shapes too (round 6; A/B)
 # GroupNorm moments from the producing conv (round 6, c2d_conv_desc::gn_mom): norm2 of every ResnetBlock2D and
 # the norm after a resnet read the statistics its row-ring conv emitted (one GroupNorm launch instead of two);
 # C2D_GN_MOMENTS=0 (A/B) keeps the statistics pass
@@ -187,10 +188,20 @@ class BasicTransformerBlock(nn.Module):
         """Fold the LayerNorm into this GEMM: where the planner runs it on the panel kernel anyway,
         and at K = 320 from 8192 rows on, where the folded panel GEMM beats LayerNorm + the
         planner's tile on every UNet shape measured (profiles/r05_ln_fold.txt: to_q 320 -> 320 at
-        c3 42.8 -> 34.7 us, c5's fused QKV 105.9 -> 92.4); at K = 640 only the panel shapes gain."""
+        c3 42.8 -> 34.7 us, c5's fused QKV 105.9 -> 92.4); at K = 640 (one 160-KiB panel workgroup
+        per CU) from 8192 rows where the panels x column splits fit one round of 256 CUs (c3 level 1:
+        QKV 66.7 -> 65.8, to_q 34.4 -> 32.3 us before the LayerNorm launch's in-situ gap; c5's
+        18432 rows take 288 workgroups and lose: 76.2 -> 115.3)."""
         c = self.norm1.c
-        return (self.lnf_folded and ops.panel_gemm(m, c, cout, geglu, lnfold=True)
-                and (ops.panel_gemm(m, c, cout, geglu) or (c == 320 and m >= 8192)))
+        if not (self.lnf_folded and ops.panel_gemm(m, c, cout, geglu, lnfold=True)):
+            return False
+        if ops.panel_gemm(m, c, cout, geglu) or (c == 320 and m >= 8192):
+            return True
+        if c == 640 and m >= 8192 and FOLD_LN640:
+            panels = (m + 127) // 128
+            ns = min(max((256 + panels - 1) // panels, 1), ((cout >> 5) + 7) // 8)   # igemm_panel.h panel_nsplit
+            return panels * ns <= 256
+        return False
 
     def _attend(self, attn: Attention, x, h, ehs, mask, kwargs):
         if getattr(attn.processor, "fuses_residual", False):
