@@ -24,6 +24,14 @@ namespace c2d {
 #define C2D_TUNE_ATTN_BUFLD 1   // whole key tiles staged by buffer loads off a per-tile SGPR base (round 6); 0 = A/B builds
 #endif
 
+#ifndef C2D_TUNE_ATTN_W8_MIN
+// d = 40: the 8-wave (256-query) blocks only when the grid has at least this many of them (one per CU); a
+// smaller grid runs 4-wave blocks, twice as many (round 6, scripts/bench_attn.py, same box: c2's CFG-shared
+// first self-attention, 8 heads x 16 blocks, 69.6 / 68.2 -> 53.4 / 55.4 us; at 256 blocks, c2's 16 heads,
+// the 8-wave form stays ahead, 77.9 vs 80.9 us); 0 = always 8-wave (A/B builds)
+#define C2D_TUNE_ATTN_W8_MIN 256
+#endif
+
 #ifndef C2D_TUNE_ATTN80
 #define C2D_TUNE_ATTN80 1   // d = 80: 1 = the PV row-sum column (round 6), 0 = VALU row sums (round 5; A/B builds)
 #endif
@@ -849,8 +857,8 @@ static int launch_attn(const void* q, int ldq, const void* k, int ldk, const voi
     if constexpr (D == 40) {
         // 8-wave blocks (256 queries): one K / V staging chunk per thread instead of two
         // (L0: 586-628 -> 560-594 us, same box); d = 80 measured 72 -> 76 us with them
-        if (lk % 64 == 0 && lk >= 256 && attn_negc() && attn_w8()) {
-            const int nqb8 = (lq + 255) / 256;
+        const int nqb8 = (lq + 255) / 256;
+        if (lk % 64 == 0 && lk >= 256 && attn_negc() && attn_w8() && nqb8 * batch * heads >= C2D_TUNE_ATTN_W8_MIN) {
             hipLaunchKernelGGL((attn_fwd_kernel<D, false, true, false, false, 8>), dim3(nqb8 * batch * heads),
                                dim3(512), smem, s, (const f16*)q, ldq, (const f16*)k, ldk, (const f16*)v, ldv, (f16*)o,
                                ldo, heads, lq, lk, scale * 1.4426950408889634f, kv_div, nqb8, attn_abl());

@@ -786,12 +786,15 @@ def test_attention_wide_scores(dev, d):
     close(out, ref)
 
 
-@pytest.mark.parametrize("lq,lk,scale", [(300, 256, 1.0), (192, 320, 12.0), (520, 1024, 4.0)])
-def test_attention_d40_w8(dev, lq, lk, scale):
-    """The 8-wave d = 40 kernel (lk % 64 == 0, lk >= 256, no mask): a ragged last 256-query block,
-    and scores of std ~12 / ~4 so the first tile rebases the running max and later tiles rescale
-    (the lazy 2^8 test)."""
-    b, h, d = 2, 4, 40
+@pytest.mark.parametrize("b,h,lq,lk,scale", [
+    (4, 8, 2000, 256, 1.0), (4, 8, 1800, 320, 12.0), (4, 8, 2040, 1024, 4.0),   # 8-wave blocks (>= 256 of them)
+    (2, 4, 300, 256, 1.0), (2, 4, 520, 1024, 4.0),                            # small grids: 4-wave NEGC blocks
+])
+def test_attention_d40_w8(dev, b, h, lq, lk, scale):
+    """The 8-wave d = 40 kernel (lk % 64 == 0, lk >= 256, no mask, a grid of >= 256 such blocks) and its 4-wave
+    twin below that: a ragged last query block, and scores of std ~12 / ~4 so the first tile rebases the
+    running max and later tiles rescale (the lazy 2^8 test)."""
+    d = 40
     q = gen(b * lq, h * d, seed=47) * scale
     k = gen(b * lk, h * d, seed=48)
     v = gen(b * lk, h * d, seed=49)
