@@ -24,6 +24,9 @@ namespace c2d {
 #define C2D_TUNE_ATTN_BUFLD 1   // whole key tiles staged by buffer loads off a per-tile SGPR base (round 6); 0 = A/B builds
 #endif
 
+#ifndef C2D_TUNE_ATTN_PRIO
+#define C2D_TUNE_ATTN_PRIO 0
+#endif
 #ifndef C2D_TUNE_ATTN_W8_MIN
 // d = 40: the 8-wave (256-query) blocks only when the grid has at least this many of them (one per CU); a
 // smaller grid runs 4-wave blocks, twice as many (round 6, scripts/bench_attn.py, same box: c2's CFG-shared
@@ -137,6 +140,9 @@ attn_fwd_kernel(const f16* __restrict__ q, int ldq, const f16* __restrict__ k,
     char* Vs = smem + C::K_BYTES;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // 8-wave blocks: static priority for the second-dispatched half (waves 4-7), the VALU-issue
+    // arbitration loser of each SIMD pair (C2D_TUNE_ATTN_PRIO, A/B)
+    if (C2D_TUNE_ATTN_PRIO && NWV == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int qpb_ = RES ? qpb : 1;   // streaming form: one query block (a single-trip loop below)
     const int ngrp = (nqb + qpb_ - 1) / qpb_;

@@ -74,6 +74,12 @@ extern thread_local int g_last_hip_error;
 #ifndef C2D_TUNE_PANEL_STAGGER
 #define C2D_TUNE_PANEL_STAGGER 2    // panel GEMM: late start of waves 4-7, x 2048 cycles
 #endif
+#ifndef C2D_TUNE_PANEL_CARRY
+#define C2D_TUNE_PANEL_CARRY 1      // K = 320 GEGLU panel GEMM runs each block's epilogue inside the next block's K loop
+#endif
+#ifndef C2D_TUNE_PANEL_PRIO
+#define C2D_TUNE_PANEL_PRIO 1       // panel GEMM waves 4-7 at s_setprio 1
+#endif
 #ifndef C2D_TUNE_ATTN_NEGC
 #define C2D_TUNE_ATTN_NEGC 1
 #endif

@@ -195,6 +195,7 @@ __global__ void __launch_bounds__(512) igemm_panel_kernel(IgemmParams p, int nsp
         __syncthreads();
     }
     if (j0 >= nblk) return;   // wave-uniform; no barrier follows
+    if (C2D_TUNE_PANEL_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);   // static priority, waves 4-7 (A/B)
 
     int fa0[2];
 #pragma unroll
@@ -362,6 +363,7 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
     // every wave of the chip storing at once
     if (wave >= 4)
         for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(32);
+    if (C2D_TUNE_PANEL_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);   // static priority, waves 4-7 (A/B)
     int sbi = 0;   // stamp block index (diagnostic builds)
     (void)sbi;
 
@@ -381,6 +383,22 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
     };
     aread(0, fa[0]);
     int par = 0;   // ring slot of the block's step 0 (5 steps per block: it alternates)
+    // CARRY (GEGLU, C2D_TUNE_PANEL_CARRY): a block's epilogue runs inside the next block's K loop,
+    // one 16-row tile per K half-step (steps 0-7 of 10) among that step's MFMAs, from the previous
+    // block's accumulators kept in registers; the last block's is flushed after the loop.  Every
+    // carried half-step issues one store, so the counted waits of the steps after it allow one more
+    constexpr bool CARRY = C2D_TUNE_PANEL_CARRY && EPI == PE_GEGLU;
+    f32x4 accp[2][8];
+    int jprev = 0;
+    const __amdgpu_buffer_rsrc_t rout = make_rsrc(p.out, (unsigned)((size_t)p.M * p.out_ld * 2));
+    auto carry_row = [&](int b) __attribute__((always_inline)) {
+        const int m = m0 + b * 16 + (lane & 15);
+        const unsigned off = m < p.M ? (unsigned)(2 * (m * p.out_ld + 16 * jprev + 4 * (lane >> 4))) : kOOB;
+        f16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (f16)(accp[0][b][r] * gelu_sig(accp[1][b][r]));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rout, off, 0, 0);
+    };
     auto block = [&](int j, bool first) __attribute__((always_inline)) {
         C2D_PSTAMP(2 + 8 * sbi);
         const int jn = j + stride < nblk ? j + stride : j;
@@ -406,10 +424,14 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
                     }
                 }
                 bdma(jn, 0, (par + NKB) & 1);
-                panel_wait_vm<4 + NRES>();
+                if (CARRY && !first) panel_wait_vm<4 + NRES + 2>();
+                else panel_wait_vm<4 + NRES>();
             } else {
                 bdma(j, t + 1, (par + t + 1) & 1);
-                if (t == 0 && !first) panel_wait_vm<4 + NST>();
+                if (CARRY) {
+                    if (t > 0 && !first) panel_wait_vm<4 + 2>();
+                    else panel_wait_vm<4>();
+                } else if (t == 0 && !first) panel_wait_vm<4 + NST>();
                 else panel_wait_vm<4>();
             }
             C2D_PSTAMP(3 + 8 * sbi + t);
@@ -423,6 +445,7 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
             for (int h = 0; h < 2; ++h) {
                 const int ks = 2 * t + h;
                 aread(ks + 1 < 2 * NKB ? ks + 1 : 0, fa[(ks + 1) & 1]);
+                if (CARRY && !first && ks < 8) carry_row(ks);
 #pragma unroll
                 for (int b = 0; b < 8; ++b) {
                     acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[h][0], fa[ks & 1][b], acc[0][b], 0, 0, 0);
@@ -432,13 +455,25 @@ __global__ void __launch_bounds__(512) igemm_panel_dma_kernel(IgemmParams p, int
             }
         }
         C2D_PSTAMP(8 + 8 * sbi);
-        panel_epilogue<EPI>(p, acc, rv, m0, 32 * j, lane);
+        if constexpr (CARRY) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 8; ++b) accp[a][b] = acc[a][b];
+            jprev = j;
+        } else {
+            panel_epilogue<EPI>(p, acc, rv, m0, 32 * j, lane);
+        }
         C2D_PSTAMP(9 + 8 * sbi);
         ++sbi;
         par ^= 1;
     };
     block(j0, true);
     for (int j = j0 + stride; j < nblk; j += stride) block(j, false);
+    if constexpr (CARRY) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) carry_row(b);
+    }
     panel_wait_vm<0>();   // the last block's look-ahead pieces land before the workgroup's LDS is released
 }
 

@@ -41,7 +41,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
       norm) arm "$label" "$envs" timeout -k 10 120 python -u scripts/bench_norm_graph.py 2>&1 | grep -E "^(GN|LN)" || exit 1 ;;
       attn) arm "$label" "$envs" timeout -k 10 200 python -u scripts/bench_attn.py 2>&1 | grep -v "amdgpu.ids\|^\[W" || exit 1 ;;
       shapes) arm "$label" "$envs" timeout -k 10 300 python -u scripts/unet_shapes.py 2>&1 | grep -v "amdgpu.ids\|^\[W" \
-                | head -${SHAPES_LINES:-24} || exit 1 ;;
+                | sed -n "1,${SHAPES_LINES:-24}p" || exit 1 ;;
       bench) arm "$label" "$envs" timeout -k 10 400 python -u bench.py $BENCH_ARGS > gpurun_out/ab/${label}_$r.json \
                2> gpurun_out/ab/${label}_$r.err || { tail -5 gpurun_out/ab/${label}_$r.err; exit 1; }
              python3 - gpurun_out/ab/${label}_$r.json <<'PY'

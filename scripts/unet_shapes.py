@@ -43,7 +43,7 @@ _conv = ops.conv
 def rec(*args, **kw):
     out = _conv(*args, **kw)
     kw = dict(kw)
-    kw["out"] = out
+    kw["out"] = out[0] if isinstance(out, tuple) else out   # (out, GnMoments) when gn_moments > 0
     calls.append((args, kw))
     return out
 

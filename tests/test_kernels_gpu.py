@@ -412,7 +412,10 @@ def test_panel_gemm_forced(dev, force_plan, m, cin, cout, res):
     close(out, ref)
 
 
-@pytest.mark.parametrize("m,cin,inner", [(2048, 320, 1280), (777, 640, 2560)])
+@pytest.mark.parametrize("m,cin,inner", [
+    (2048, 320, 1280), (777, 640, 2560),
+    (8100, 320, 1280),   # 64 panels x 4 column splits: 5 column blocks per wave (the carried epilogue's steady state), ragged last panel
+])
 def test_panel_gemm_forced_geglu(dev, force_plan, m, cin, inner):
     force_plan(70, 0)
     x = gen(m, cin, seed=105)
